@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark of the Gaussian / DoG pyramid build on MI355X — BASELINE.json's metric:
+"Mpix/s full Gaussian+DoG pyramid build; % HBM roofline at 1/2/4/8 GPU".
+
+A step is one fused pyramid build (GaussPyInit + GenerateDoG of GuassDePyramid.h, S = 2,
+5 octaves) over each rank's resident batch of synthetic int32 images, through the C ABI
+(libgdp.so, one kernel launch per step).  Input pixels are generated on each GPU before the timed
+region; nothing leaves HBM inside it.  One process per GPU (torchrun), ranks shard the images
+(no data-path collective: images are independent), max-over-ranks timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+Workloads (BASELINE.json configs; c2 is the default, the single-GPU config the metric names):
+  c2: 4096x4096, 5 octaves, 1 image per GPU per step
+  c3: 64 x 1080x1920 (HxW), 5 octaves, per GPU per step (persistent kernel)
+  c4: 64 x 4096x4096, 5 octaves, per GPU per step (MPI-variant image sharding)
+  c5: 16384x16384, 5 octaves, ONE image split into row bands across the ranks
+Prints ONE JSON line on rank 0 (contract in the task description).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mpix/s full Gaussian+DoG pyramid build; % HBM roofline at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+SEED = 0x5EED
+
+CONFIGS = {
+    "c2": dict(H=4096, W=4096, batch=1, O=5, band=False, name="1xMI355X 4096x4096 image, 5 octaves x 5 scales"),
+    "c3": dict(H=1080, W=1920, batch=64, O=5, band=False, name="batch of 64 x 1920x1080 images, 5 octaves x 5 scales"),
+    "c4": dict(H=4096, W=4096, batch=64, O=5, band=False, name="64 x 4096x4096 images per GPU, 5 octaves x 5 scales"),
+    "c5": dict(H=16384, W=16384, batch=1, O=5, band=True, name="16384x16384 single image in row bands, 5 octaves"),
+}
+
+
+def pyramid_pixels(H, W, O, rows=None):
+    """P = sum over octaves of rows_o * cols_o."""
+    return sum(((rows if rows is not None else H) >> o) * (W >> o) for o in range(O))
+
+
+def algorithmic_bytes(H, W, S, O, batch):
+    """B = 4*H*W (read every input pixel once) + 4*(S+3)*P (write the final pyramid once)."""
+    return batch * (4 * H * W + 4 * (S + 3) * pyramid_pixels(H, W, O))
+
+
+def cpu_info():
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def host_threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(budget_s):
+    """The reference's AVX512xOpenMP path (GaussDePyramid-AVX512xOpenMP.h:240-364) on the host cores,
+    timed on a bounded sample: 4096x4096 image (the c2 workload's input), all its octaves, reps
+    sized to ~budget_s.  Falls back to the oracle's restatement ("port") when oracle/_ref is absent
+    or the host lacks AVX-512.  Uses the oracle only as the CPU baseline, never on the GPU path."""
+    import __graft_entry__ as entry
+
+    oracle = entry.load_oracle()
+    n, S = 4096, 2
+    threads = host_threads()
+    spec = f"synth:{SEED:#x}:0"
+    if oracle.ref_binary("avx512") and oracle.host_has_avx512():
+        probe = oracle.ref_time("time-a512omp", n, S, spec, 2, threads)
+        reps = max(3, min(400, int(budget_s / max(probe["ms_median"] / 1e3, 1e-4))))
+        rec = oracle.ref_time("time-a512omp", n, S, spec, reps, threads)
+        serial = oracle.ref_time("time-serial", n, S, spec, 2) if oracle.ref_binary("serial") else None
+        out = {
+            "value": round(n * n / (rec["ms_median"] / 1e3) / 1e6, 3), "unit": "Mpix/s", "cores": threads,
+            "kind": "reference",
+            "sample": (f"GaussPyramid_a512omp::GenerateDoG_nomp_dynamic (reference header compiled in place, "
+                       f"counnt={threads}) on one {n}x{n} synthetic image, all {rec['octaves']} octaves, "
+                       f"median of {rec['reps']} calls after a warm-up; GaussPyInit untimed as in the reference. "
+                       f"NB: that path filters only S of the S+3 scales and forms 1 of the S+2 DoG levels "
+                       f"(~34% of the full build's bytes)"),
+            "cpu": cpu_info(),
+        }
+        if serial:
+            out["serial_full_semantics"] = {"value": round(n * n / (serial["ms_median"] / 1e3) / 1e6, 3),
+                                            "unit": "Mpix/s", "cores": 1,
+                                            "sample": f"GuassDePyramid.h GenerateDoG, {n}x{n}, median of {serial['reps']}"}
+        return out
+    import numpy as np
+
+    img = oracle.synthetic_image(n, n, SEED, 0)
+    base = oracle.init_pyramid(img, S)
+    O = oracle.octaves(n)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while time.perf_counter() < t_end or len(times) < 3:
+        pyr = base.copy()
+        t0 = time.perf_counter()
+        oracle.subset_a512omp(pyr, n, n, S, O)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": round(n * n / med / 1e6, 3), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"oracle restatement of GenerateDoG_nomp_dynamic (OpenMP, {threads} threads), {n}x{n}, "
+                      f"median of {len(times)} calls", "cpu": cpu_info()}
+
+
+def latest_pmc(config_key):
+    """PMC-derived HBM bytes per launch for this workload, from profiles/pmc_*.json (written by
+    profiles/collect_pmc.py from separate rocprofv3 --pmc passes), or None."""
+    pdir = os.path.join(REPO, "profiles")
+    best = None
+    if os.path.isdir(pdir):
+        for f in sorted(os.listdir(pdir)):
+            if f.startswith("pmc_") and f.endswith(".json"):
+                try:
+                    with open(os.path.join(pdir, f)) as fh:
+                        rec = json.load(fh)
+                except (OSError, ValueError):
+                    continue
+                if rec.get("config") == config_key and rec.get("kernel_bytes_per_launch"):
+                    best = rec
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="override images per GPU")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
+    H, W, S, O, B = cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"]
+    if cfg["band"]:
+        # one image, row bands aligned to 2^(O-1) rows: each rank owns rows [r0, r1)
+        align = 1 << (max(O, 5) - 1)
+        per = -(-H // world // align) * align
+        r0, r1 = min(H, rank * per), min(H, (rank + 1) * per)
+        ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=1, device=local, row_begin=r0, row_end=r1)
+        ctx.fill_synthetic(SEED, 0)
+        scaling = "strong"
+        units_all = H * W  # input pixels of the whole job per step
+    else:
+        ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, device=local)
+        ctx.fill_synthetic(SEED, rank * B)  # rank r owns global images [r*B, (r+1)*B)
+        scaling = "weak"
+        units_all = world * B * H * W
+    ctx.sync()
+    stream = torch.cuda.current_stream()
+
+    for _ in range(args.warmup):
+        ctx.build(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        ctx.build(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
+    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kernel_ms = float(t[0]), float(t[1])
+
+    # roofline of the (only) kernel of a step, per launch on THIS rank's share
+    rows_local = ctx.row_end - ctx.row_begin
+    if cfg["band"]:
+        bytes_launch = 4 * rows_local * W + 4 * (S + 3) * sum(ctx.level_dims(o)[0] * ctx.level_dims(o)[1] for o in range(O))
+    else:
+        bytes_launch = algorithmic_bytes(H, W, S, O, B)
+    achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
+    pmc = latest_pmc(args.config)
+
+    result = {
+        "metric": METRIC,
+        "value": round(units_all * args.steps / wall / 1e6, 3),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 6),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (on-device counter-hash int32 images, SURVEY.md §8d)",
+        "config": {
+            "workload": cfg["name"], "H": H, "W": W, "S": S, "octaves": O, "scales": S + 3,
+            "images_per_gpu": 1 if cfg["band"] else B,
+            "parallelism": (f"row-band x{world}" if cfg["band"] else f"image-sharded x{world}"),
+            "input_mpix_per_step": units_all / 1e6,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": round(pmc["kernel_bytes_per_launch"]) if pmc else None,
+            "kernel": "k_build<5,true> (fused decimate+window+DoG)",
+            "kernel_ms": round(kernel_ms, 6),
+            "algorithmic_bytes_per_launch": bytes_launch,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+// GaussDePyramid-HIP.h — drop-in MI355X replacement for the reference's pyramid classes.
+//
+// Usage is the reference's own (main.cpp:2-13, 61-74): swap the #include line and the class name,
+//     #include "GaussDePyramid-HIP.h"
+//     GaussPyramid_hip g(p, n, 2);
+//     g.GenerateDoG();            // GaussFilter + DoG of every octave on the GPU
+//     g.GaussPy[o][s][r][c] ...   // host float**** mirror, as in GuassDePyramid.h:16
+// and link with -lgdp (libgdp.so, sift-parallel-optimization_amd/lib).  The class mirrors
+// `class GaussPyramid` (GuassDePyramid.h:11-29) member for member; every method is a thin
+// caller of the C ABI in gdp.h.  Host code only: this header needs no HIP headers and compiles
+// with plain g++.
+//
+// Semantics kept from the reference:
+//  - the constructor deep-copies img[0:len][0:len] and calls GaussPyInit() (:36-58);
+//  - GaussPyInit() refills every level with the decimated input (:60-87);
+//  - GaussFilter(o) window-multiplies every scale of octave o in place (:106-134);
+//  - GenerateDoG() = GaussFilter + DoG per octave on the CURRENT contents (:136-149), so calling
+//    it twice without GaussPyInit() filters twice, like the timing loop of main.cpp:66-73;
+//  - GaussPy holds [layer][S+3][len_o][len_o] floats allocated with new[] (:63-72), freed by the
+//    destructor (:151-170).
+// Differences: the reference never reports errors; a failing libgdp call here prints
+// gdp_last_error() and aborts rather than continuing on bad state.  After each mutating call
+// the device pyramid is copied back into GaussPy (PCIe traffic of the whole pyramid) unless
+// `mirror_host` is set to false, in which case call SyncHost() before reading GaussPy.
+#ifndef SIFT_GAUSSDEPYRAMID_HIP_H
+#define SIFT_GAUSSDEPYRAMID_HIP_H
+
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+
+#include "gdp.h"
+
+class GaussPyramid_hip {
+public:
+    int** data;  // copy of the input image (:13)
+    GaussPyramid_hip();
+    GaussPyramid_hip(int** img, int len, int S, int device = 0);
+    float**** GaussPy;  // [layer][S+3][len_o][len_o] host mirror (:16)
+    void GaussPyInit();
+    void output();
+    void GaussFilter(int theLayer);
+    void GenerateDoG();
+    ~GaussPyramid_hip();
+    bool initialized;
+    bool mirror_host;  // copy the pyramid into GaussPy after every mutating call (default true)
+    void SyncHost();   // copy the device pyramid into GaussPy now
+    gdp_ctx* context() const { return ctx_; }
+
+protected:
+    int length;
+    int S;
+    int layer;
+    float* filter;  // unused (taps live on the device); kept for layout parity with :28
+    gdp_ctx* ctx_;
+    bool fresh_;  // contents == GaussPyInit(): GenerateDoG may use the fused build kernel
+    static void check_(gdp_ctx* c, int status, const char* what) {
+        if (status != GDP_OK) {
+            std::fprintf(stderr, "GaussPyramid_hip::%s failed: %s (%s)\n", what, gdp_status_string(status),
+                         gdp_last_error(c));
+            std::abort();
+        }
+    }
+};
+
+inline GaussPyramid_hip::GaussPyramid_hip()
+    : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), length(0), S(0), layer(0),
+      filter(nullptr), ctx_(nullptr), fresh_(false) {}
+
+inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device)
+    : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), length(len), S(S_), layer(0),
+      filter(nullptr), ctx_(nullptr), fresh_(false) {
+    data = new int*[len];
+    for (int i = 0; i < len; ++i) {
+        data[i] = new int[len];
+        for (int j = 0; j < len; ++j) data[i][j] = img[i][j];
+    }
+    layer = gdp_octaves_for(len);  // :48-53
+    filter = new float[len];
+    check_(nullptr, gdp_create(&ctx_, len, len, S, layer, 1, device), "GaussPyramid_hip");
+    check_(ctx_, gdp_set_input_rows(ctx_, 0, (const int32_t* const*)data, nullptr), "GaussPyramid_hip");
+    GaussPy = new float***[layer];
+    for (int o = 0; o < layer; ++o) {
+        const int n = len >> o;
+        GaussPy[o] = new float**[S + 3];
+        for (int s = 0; s < S + 3; ++s) {
+            GaussPy[o][s] = new float*[n];
+            for (int r = 0; r < n; ++r) GaussPy[o][s][r] = new float[n];
+        }
+    }
+    GaussPyInit();
+}
+
+inline void GaussPyramid_hip::SyncHost() {
+    for (int o = 0; o < layer; ++o)
+        for (int s = 0; s < S + 3; ++s)
+            check_(ctx_, gdp_download_level_rows(ctx_, 0, o, s, GaussPy[o][s]), "SyncHost");
+}
+
+inline void GaussPyramid_hip::GaussPyInit() {
+    check_(ctx_, gdp_init(ctx_, nullptr), "GaussPyInit");
+    initialized = true;
+    fresh_ = true;
+    if (mirror_host) SyncHost();
+}
+
+inline void GaussPyramid_hip::GaussFilter(int theLayer) {
+    check_(ctx_, gdp_gauss_octave(ctx_, theLayer, nullptr), "GaussFilter");
+    fresh_ = false;
+    if (mirror_host) SyncHost();
+}
+
+inline void GaussPyramid_hip::GenerateDoG() {
+    // on freshly initialised contents the fused single-pass build is bit-identical to
+    // GaussFilter + DoG in place; otherwise run the in-place pass on what is there
+    check_(ctx_, fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr), "GenerateDoG");
+    fresh_ = false;
+    check_(ctx_, gdp_sync(ctx_), "GenerateDoG");
+    if (mirror_host) SyncHost();
+}
+
+inline void GaussPyramid_hip::output() {  // :89-104
+    int len = length;
+    for (int i = 0; i < layer; ++i) {
+        for (int j = 0; j < len; ++j) {
+            for (int k = 0; k < len; ++k) std::cout << GaussPy[i][0][j][k] << " ";
+            std::cout << std::endl;
+        }
+        for (int k = 0; k < len; ++k) std::cout << "==";
+        std::cout << std::endl;
+        len /= 2;
+    }
+}
+
+inline GaussPyramid_hip::~GaussPyramid_hip() {
+    if (GaussPy) {
+        for (int o = 0; o < layer; ++o) {
+            for (int s = 0; s < S + 3; ++s) {
+                for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
+                delete[] GaussPy[o][s];
+            }
+            delete[] GaussPy[o];
+        }
+        delete[] GaussPy;
+    }
+    if (data) {
+        for (int i = 0; i < length; ++i) delete[] data[i];
+        delete[] data;
+    }
+    delete[] filter;
+    gdp_destroy(ctx_);
+}
+
+#endif  // SIFT_GAUSSDEPYRAMID_HIP_H

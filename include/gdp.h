@@ -1,0 +1,152 @@
+/*
+ * gdp.h — C ABI of libgdp.so, the MI355X (gfx950) Gaussian / Difference-of-Gaussians pyramid.
+ *
+ * This is the drop-in boundary for the reference's pyramid hot path
+ * (ZhangShuui/SIFT-parallel-optimization, GuassDePyramid.h and the GaussDePyramid-*.h variants).
+ * The reference exposes a duck-typed C++ class surface selected by #include (main.cpp:2-13);
+ * every entry point below names the reference member it replaces (file:line).  The C++ class
+ * `GaussPyramid_hip` (include/GaussDePyramid-HIP.h) and the Python mirror
+ * (sift-parallel-optimization_amd/gausspyramid.py) are thin callers of exactly these functions.
+ *
+ * Conventions
+ *  - Every function returns an int status (GDP_OK == 0) unless documented otherwise; no C++
+ *    exception crosses the ABI.  gdp_last_error(ctx) / gdp_status_string() describe failures.
+ *  - Only plain pointers and sizes cross the boundary.  `stream` is a hipStream_t passed as
+ *    void* (NULL = the context's own stream); all compute and copy calls are stream-ordered and
+ *    asynchronous unless documented otherwise.
+ *  - The context owns its device buffers (input, pyramid, tap tables); the caller keeps
+ *    ownership of every host array it passes in.  One context per host thread and device.
+ *  - Semantics are the reference's, bit for bit: float32 taps from glibc expf/sqrtf computed on
+ *    the host (GuassDePyramid.h:119-121), products ((float)x * f[c]) * f[r] with no FMA
+ *    contraction and denormals kept, DoG_s = G_s - G_{s+1} in ascending s (:140-146),
+ *    level S+2 keeps the last Gaussian.
+ *
+ * Pyramid geometry (per image b of a batch):
+ *   octave o has rows_o x cols_o pixels, cols_o = W >> o and (whole image) rows_o = H >> o;
+ *   scale s in [0, S+3).  Octave o decimates the ORIGINAL image: input pixel (r<<o, c<<o)
+ *   (GuassDePyramid.h:80).  `octaves` = 0 selects floor(log2(min(H, W))) + 1, the reference's
+ *   `layer` (GuassDePyramid.h:48-53).  The reference is square-only; H != W is an extension
+ *   (W-derived window along columns, H-derived window along rows).
+ *   A "band" context computes the output rows whose input rows lie in [row_begin, row_end) of
+ *   an H-row image (multi-GPU row-band partition; the operation is pointwise, halo = 0).
+ */
+#ifndef GDP_H_
+#define GDP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gdp_ctx gdp_ctx;
+
+enum {
+    GDP_OK = 0,
+    GDP_ERR_ARG = 1,      /* invalid argument (sizes, indices, null pointers)        */
+    GDP_ERR_HIP = 2,      /* a HIP runtime call failed (message in gdp_last_error)   */
+    GDP_ERR_STATE = 3,    /* call not valid in the context's current state           */
+    GDP_ERR_NOMEM = 4,    /* host or device allocation failed                        */
+    GDP_ERR_NODEV = 5     /* no usable gfx950 device                                 */
+};
+
+/* ABI version of this header; gdp_abi_version() returns the library's. */
+#define GDP_ABI_VERSION 1
+int gdp_abi_version(void);
+
+/* Number of octaves the reference builds for an n-pixel axis: floor(log2 n) + 1
+ * (GaussPyramid ctor, GuassDePyramid.h:48-53). */
+int gdp_octaves_for(int n);
+
+/* Allocate a context for `batch` images of H x W int32 pixels, S (+3 Gaussian scales per octave)
+ * and `octaves` octaves (0 = all) on HIP device `device`, and upload the tap tables.
+ * Replaces the allocation half of GaussPyramid(int** img, int len, int S)
+ * (GuassDePyramid.h:36-58) and GaussPyInit's first-call allocation (:60-73). */
+int gdp_create(gdp_ctx** out, int height, int width, int S, int octaves, int batch, int device);
+
+/* Same as gdp_create for the row band [row_begin, row_end) of an H-row image.  row_begin must
+ * be a multiple of 2^(max(octaves,5)-1); row_end must be too, or equal `height`.  Extension for
+ * the multi-GPU row-band split (no reference counterpart). */
+int gdp_create_band(gdp_ctx** out, int height, int width, int S, int octaves, int batch, int row_begin,
+                    int row_end, int device);
+
+/* Free every device buffer.  Replaces ~GaussPyramid() (GuassDePyramid.h:151-170). */
+void gdp_destroy(gdp_ctx* ctx);
+
+/* Geometry queries.  gdp_level_dims gives the rows held by this context for octave o (the whole
+ * image, or the band), their first global row, and the columns. */
+int gdp_get_geometry(const gdp_ctx* ctx, int* height, int* width, int* S, int* octaves, int* batch);
+int gdp_level_dims(const gdp_ctx* ctx, int octave, int* rows, int* cols, int* first_row);
+size_t gdp_pyramid_bytes(const gdp_ctx* ctx); /* device bytes of all pyramids of the batch */
+
+/* ---- input ---------------------------------------------------------------------------------
+ * The reference deep-copies `int** img` in its constructor (GuassDePyramid.h:38-46).  These
+ * upload image b of the batch (band contexts: the band's rows only, given as rows of the band). */
+/* int** row-pointer form, exactly the reference ctor's argument. */
+int gdp_set_input_rows(gdp_ctx* ctx, int b, const int32_t* const* rows, void* stream);
+/* contiguous host image with a row pitch of `pitch` int32 elements. */
+int gdp_set_input_host(gdp_ctx* ctx, int b, const int32_t* base, size_t pitch, void* stream);
+/* Zero-copy: read every image straight from caller-owned DEVICE memory.  Image b, row r starts
+ * at base + b*image_stride + r*pitch (int32 elements).  Pass base = NULL to go back to the
+ * context's own input buffer.  The memory must stay valid while builds run. */
+int gdp_set_input_device(gdp_ctx* ctx, const int32_t* base, size_t pitch, size_t image_stride);
+/* Benchmark/test input generated on the device (SURVEY.md §8d counter hash): image b of the
+ * batch gets global index first_image + b; pixel = lowbias32(seed ^ fold(idx)) >> 24 with
+ * idx = (index*H + r)*W + c over the WHOLE image (band contexts generate their rows only). */
+int gdp_fill_synthetic(gdp_ctx* ctx, uint32_t seed, long first_image, void* stream);
+
+/* ---- compute ------------------------------------------------------------------------------- */
+/* Fused GaussPyInit() + GenerateDoG() for every image of the batch in one launch: reads each
+ * input pixel once and writes the final pyramid once.  Equivalent, bit for bit, to
+ * GuassDePyramid.h:74-86 followed by :136-149. */
+int gdp_build(gdp_ctx* ctx, void* stream);
+/* GaussPyInit() refill: every scale of octave o := (float) decimated input
+ * (GuassDePyramid.h:74-86). */
+int gdp_init(gdp_ctx* ctx, void* stream);
+/* GaussFilter(o) in place: every scale of octave o *= column window then row window
+ * (GuassDePyramid.h:106-134). */
+int gdp_gauss_octave(gdp_ctx* ctx, int octave, void* stream);
+/* DoG of octave o in place: level s -= level s+1 for s = 0..S+1 ascending
+ * (GuassDePyramid.h:140-146). */
+int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);
+/* GenerateDoG() in place on the CURRENT contents, all octaves in one launch
+ * (GuassDePyramid.h:136-149).  After gdp_init this equals gdp_build; called again it re-filters,
+ * like the reference's repeated-call timing loop (main.cpp:66-73). */
+int gdp_generate_dog(gdp_ctx* ctx, void* stream);
+
+/* ---- output -------------------------------------------------------------------------------- */
+/* Device pointer to level (o, s) of image b: rows x cols float32, row-major, dense. */
+const float* gdp_device_level(const gdp_ctx* ctx, int b, int octave, int scale);
+/* Copy level (o, s) of image b to a dense host array (blocking). */
+int gdp_download_level(gdp_ctx* ctx, int b, int octave, int scale, float* host);
+/* Copy level (o, s) of image b into host row pointers — materialises the reference's
+ * float**** GaussPy[o][s] rows (GuassDePyramid.h:16) (blocking). */
+int gdp_download_level_rows(gdp_ctx* ctx, int b, int octave, int scale, float* const* rows);
+/* Copy the whole pyramid of image b in the packed layout [o][s][rows][cols] (blocking). */
+int gdp_download_pyramid(gdp_ctx* ctx, int b, float* host);
+/* Upload a packed pyramid of image b (state restore; used by re-entry tests). */
+int gdp_upload_pyramid(gdp_ctx* ctx, int b, const float* host);
+/* Float elements of one image's packed pyramid (what gdp_download_pyramid writes). */
+size_t gdp_packed_floats(const gdp_ctx* ctx);
+
+/* ---- taps ---------------------------------------------------------------------------------- */
+/* The column (axis = 0, from W) or row (axis = 1, from H) window of (o, s) the context uploaded,
+ * copied to host (cols_o or rows-of-whole-image_o floats).  Lets tests pin the host taps against
+ * the reference's own (tests/golden/taps.npz). */
+int gdp_get_taps(gdp_ctx* ctx, int axis, int octave, int scale, float* host);
+
+/* ---- misc ---------------------------------------------------------------------------------- */
+int gdp_sync(gdp_ctx* ctx);                    /* wait for the context's stream */
+void* gdp_stream(const gdp_ctx* ctx);          /* the context's own hipStream_t */
+const char* gdp_last_error(const gdp_ctx* ctx); /* ctx may be NULL: last create() failure */
+const char* gdp_status_string(int status);
+/* Time `iters` back-to-back gdp_build launches on `stream` with HIP events recorded on that same
+ * stream; writes the total milliseconds.  Used by bench.py for the per-launch kernel time. */
+int gdp_time_builds(gdp_ctx* ctx, int iters, void* stream, float* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDP_H_ */

@@ -1,0 +1,111 @@
+"""ctypes binding of libgdp.so — the C ABI declared in include/gdp.h.
+
+The product path is the HIP library; there is no CPU fallback.  If libgdp.so is missing or a
+call fails, this module raises GdpError — loudly, never silently computing elsewhere.
+
+HIP runtime sharing: the PyTorch-ROCm wheel ships its own libamdhip64.so (soname
+libamdhip64.so.7).  libgdp.so needs `libamdhip64.so.7`; when torch is imported FIRST, the dynamic
+loader resolves that soname to torch's already-loaded runtime, so torch streams/events and
+libgdp launches share one HIP runtime (and one device context).  Loading libgdp first would map
+/opt/rocm's runtime and torch would later map a second one.  We therefore import torch (when it
+is installed) before dlopen-ing libgdp; GDP_NO_TORCH=1 skips that for torch-free processes.
+"""
+import ctypes
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GDP_LIBRARY", os.path.join(PKG_DIR, "lib", "libgdp.so"))
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "gdp.h")
+
+GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV = range(6)
+
+
+class GdpError(RuntimeError):
+    """A libgdp call returned a non-zero status (or the library could not be loaded)."""
+
+    def __init__(self, status, message):
+        super().__init__(f"libgdp status {status}: {message}")
+        self.status = status
+
+
+_lib = None
+
+_c_int, _c_size, _p, _c_u32, _c_long = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_long
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes); mirrors include/gdp.h one to one (tests/test_abi.py checks both ways)
+SIGNATURES = {
+    "gdp_abi_version": (_c_int, []),
+    "gdp_octaves_for": (_c_int, [_c_int]),
+    "gdp_create": (_c_int, [_pp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
+    "gdp_create_band": (_c_int, [_pp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
+    "gdp_destroy": (None, [_p]),
+    "gdp_get_geometry": (_c_int, [_p] + [ctypes.POINTER(_c_int)] * 5),
+    "gdp_level_dims": (_c_int, [_p, _c_int] + [ctypes.POINTER(_c_int)] * 3),
+    "gdp_pyramid_bytes": (_c_size, [_p]),
+    "gdp_set_input_rows": (_c_int, [_p, _c_int, _p, _p]),
+    "gdp_set_input_host": (_c_int, [_p, _c_int, _p, _c_size, _p]),
+    "gdp_set_input_device": (_c_int, [_p, _p, _c_size, _c_size]),
+    "gdp_fill_synthetic": (_c_int, [_p, _c_u32, _c_long, _p]),
+    "gdp_build": (_c_int, [_p, _p]),
+    "gdp_init": (_c_int, [_p, _p]),
+    "gdp_gauss_octave": (_c_int, [_p, _c_int, _p]),
+    "gdp_dog_octave": (_c_int, [_p, _c_int, _p]),
+    "gdp_generate_dog": (_c_int, [_p, _p]),
+    "gdp_device_level": (_p, [_p, _c_int, _c_int, _c_int]),
+    "gdp_download_level": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_download_level_rows": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_download_pyramid": (_c_int, [_p, _c_int, _p]),
+    "gdp_upload_pyramid": (_c_int, [_p, _c_int, _p]),
+    "gdp_packed_floats": (_c_size, [_p]),
+    "gdp_get_taps": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_sync": (_c_int, [_p]),
+    "gdp_stream": (_p, [_p]),
+    "gdp_last_error": (ctypes.c_char_p, [_p]),
+    "gdp_status_string": (ctypes.c_char_p, [_c_int]),
+    "gdp_time_builds": (_c_int, [_p, _c_int, _p, ctypes.POINTER(ctypes.c_float)]),
+}
+
+
+def header_functions(path=HEADER):
+    """Function names declared in include/gdp.h."""
+    with open(path) as f:
+        text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(gdp_[a-z_0-9]+)\s*\(", text)))
+
+
+def _preload_torch():
+    if os.environ.get("GDP_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401  (shares torch's HIP runtime, see module docstring)
+    except ImportError:
+        pass
+
+
+def lib():
+    """Load libgdp.so once; raise GdpError if it is absent (no fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GdpError(GDP_ERR_STATE, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                                      f"or `make -C sift-parallel-optimization_amd/csrc`")
+    _preload_torch()
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    if L.gdp_abi_version() != 1:
+        raise GdpError(GDP_ERR_STATE, "libgdp ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(status, ctx=None):
+    if status != GDP_OK:
+        L = lib()
+        msg = L.gdp_last_error(ctx)
+        raise GdpError(status, (msg or b"").decode() or L.gdp_status_string(status).decode())
+    return status

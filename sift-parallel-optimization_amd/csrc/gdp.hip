@@ -1,0 +1,767 @@
+// libgdp.so — MI355X (gfx950) Gaussian / Difference-of-Gaussians pyramid: HIP kernels + C ABI.
+//
+// Hot path replaced: GuassDePyramid.h GaussPyInit (:60-87) + GaussFilter (:106-134) +
+// GenerateDoG (:136-149) of ZhangShuui/SIFT-parallel-optimization.  The reference's "Gaussian"
+// is a rank-1 WINDOW, not a convolution: level (o, s) pixel (r, c) is
+//     G_s = ((float)img[r<<o][c<<o] * fc_{o,s}[c]) * fr_{o,s}[r]
+// (row pass with the column-index tap first, :122-126, then the column pass with the row-index
+// tap, :127-131), and the DoG is DoG_s = G_s - G_{s+1}, s ascending, level S+2 keeping G_{S+2}
+// (:140-146).  No neighbourhood, so no halo and no LDS staging: the op is a pure HBM stream —
+// read 4 B per input pixel, write 4*(S+3) B per pyramid pixel — and the kernels below are built
+// for that roofline.
+//
+// Bit-exactness contract: taps are computed on the HOST with glibc expf/sqrtf exactly
+// as GuassDePyramid.h:119-121 does and uploaded; every product/difference is a single IEEE
+// binary32 operation in the reference's order — FP contraction is disabled for this file
+// (pragma below + -ffp-contract=off in the Makefile) and f32 denormals are kept (gfx950 default
+// .amdhsa_float_denorm_mode_32 = 3; never built with -ffast-math / FTZ).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "gdp.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// geometry
+// ------------------------------------------------------------------------------------------
+constexpr int kMaxOct = 32;
+constexpr int kBlock = 256;     // 4 waves
+constexpr int kFused = 5;       // octaves 0..4 share one 16 x 256 input tile
+constexpr int kTileRows = 16;   // 2^(kFused-1): every fused octave has whole rows in a tile
+constexpr int kTileCols = 256;  // octave 0: one wave = one tile row = 64 lanes x 4 pixels
+constexpr int kLevelAlign = 64; // floats (256 B) — every level starts 16-B (and 256-B) aligned
+
+struct OctGeom {
+    int rows;             // output rows of this octave held by the context (band-local)
+    int row0;             // global output row of band-local row 0
+    int cols;             // W >> o
+    int gpr;              // groups of 4 columns per row, ceil(cols / 4)
+    long long lev_off;    // floats from an image's pyramid base to level (o, 0)
+    long long lev_stride; // floats from level (o, s) to (o, s+1)
+    int ctap;             // float offset of column taps (o, 0) in the tap table
+    int ctap_stride;      // floats between scales (multiple of 4, zero padded)
+    int rtap;             // float offset of row taps (o, 0), indexed by GLOBAL output row
+    int rtap_stride;
+    long long grp_begin;  // prefix (over octaves 0..o-1) of rows*gpr per image
+};
+
+struct Geom {
+    int H, W, S, L, O, F, batch;
+    int in_rows, in_row0; // input rows held (band) and their first global row
+    int vec_in;           // 16-B int4 input loads legal (pitch % 4 == 0, base aligned)
+    int pad_;
+    long long in_pitch, in_img_stride;
+    long long pyr_stride; // floats between image pyramids
+    int tiles_r, tiles_c;
+    long long tiles_per_img, tiles_total;
+    long long tail_groups_per_img, tail_units; // octaves >= F, 256 groups per unit
+    OctGeom oct[kMaxOct];
+};
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef int i4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ f4 ld_f4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+template <bool NT>
+__device__ __forceinline__ void st_f4(float* p, f4 v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+    else
+        *reinterpret_cast<f4*>(p) = v;
+}
+
+// Stores the first `n` lanes of v (n in 1..4) — ragged right edge or unaligned rows.
+__device__ __forceinline__ void st_part(float* p, f4 v, int n, bool aligned_full) {
+    if (aligned_full) {
+        *reinterpret_cast<f4*>(p) = v;
+        return;
+    }
+    p[0] = v.x;
+    if (n > 1) p[1] = v.y;
+    if (n > 2) p[2] = v.z;
+    if (n > 3) p[3] = v.w;
+}
+
+// Input pixels (R, C..C+3) of octave o for image b as float (zero beyond the row end).
+__device__ __forceinline__ f4 load_px(const Geom* __restrict__ g, const int* __restrict__ in, int b, int o,
+                                      int Rg, int C, int n) {
+    const long long in_row = ((long long)Rg << o) - g->in_row0;
+    const int* row = in + (long long)b * g->in_img_stride + in_row * g->in_pitch;
+    if (o == 0 && n == 4 && g->vec_in) {
+        const i4 v = *reinterpret_cast<const i4*>(row + C);
+        return __builtin_convertvector(v, f4);
+    }
+    f4 x = {0.f, 0.f, 0.f, 0.f};
+    x.x = (float)row[(long long)C << o];
+    if (n > 1) x.y = (float)row[(long long)(C + 1) << o];
+    if (n > 2) x.z = (float)row[(long long)(C + 2) << o];
+    if (n > 3) x.w = (float)row[(long long)(C + 3) << o];
+    return x;
+}
+
+// One group = 4 consecutive output pixels (Rl, C..C+3) of octave o, all S+3 scales.
+// G_s = (x * fc_s) * fr_s ; out_s = G_s - G_{s+1} ; out_{L-1} = G_{L-1}.
+template <int LT, bool NT>
+__device__ __forceinline__ void build_group(const Geom* __restrict__ g, const int* __restrict__ in,
+                                            float* __restrict__ out, const float* __restrict__ taps, int b,
+                                            int o, const OctGeom& og, int Rl, int C) {
+    const int L = LT > 0 ? LT : g->L;
+    const int n = min(4, og.cols - C);
+    const int Rg = og.row0 + Rl;
+    const f4 x = load_px(g, in, b, o, Rg, C, n);
+    const float* ct = taps + og.ctap + C;
+    const float* rt = taps + og.rtap + Rg;
+    float* dst = out + (long long)b * g->pyr_stride + og.lev_off + (long long)Rl * og.cols + C;
+    const bool full = (n == 4) && ((og.cols & 3) == 0);
+    f4 gp = (x * ld_f4(ct)) * rt[0];
+#pragma unroll
+    for (int s = 0; s + 1 < L; ++s) {
+        const f4 gn = (x * ld_f4(ct + (s + 1) * og.ctap_stride)) * rt[(s + 1) * og.rtap_stride];
+        const f4 d = gp - gn;
+        if (full)
+            st_f4<NT>(dst + s * og.lev_stride, d);
+        else
+            st_part(dst + s * og.lev_stride, d, n, false);
+        gp = gn;
+    }
+    if (full)
+        st_f4<NT>(dst + (L - 1) * og.lev_stride, gp);
+    else
+        st_part(dst + (L - 1) * og.lev_stride, gp, n, false);
+}
+
+// Fused build.  Work units: [0, tiles_total) are 16 x 256 input tiles (octaves 0..F-1 of the
+// tile: octave o covers (16>>o) rows x (256>>o) columns, reading lines the o = 0 pass of the
+// same block just brought on chip); [tiles_total, +tail_units) are 256-group slices of the tiny
+// octaves >= F.  Persistent grid-stride loop over units (grid <= 8 blocks per CU).
+template <int LT, bool NT>
+__global__ void __launch_bounds__(kBlock) k_build(const Geom* __restrict__ g, const int* __restrict__ in,
+                                                  float* __restrict__ out, const float* __restrict__ taps) {
+    const long long tiles_total = g->tiles_total;
+    const long long units = tiles_total + g->tail_units;
+    const int F = g->F;
+    for (long long u = blockIdx.x; u < units; u += gridDim.x) {
+        if (u < tiles_total) {
+            const int b = (int)(u / g->tiles_per_img);
+            const long long rem = u - (long long)b * g->tiles_per_img;
+            const int tr = (int)(rem / g->tiles_c);
+            const int tc = (int)(rem - (long long)tr * g->tiles_c);
+            const int in_r0 = tr * kTileRows; // band-local input row of the tile
+            const int in_c0 = tc * kTileCols;
+#pragma unroll
+            for (int o = 0; o < kFused; ++o) {
+                if (o >= F) break;
+                const OctGeom og = g->oct[o];
+                const int gpr_t = (kTileCols / 4) >> o; // 64, 32, 16, 8, 4
+                const int groups = (kTileRows >> o) * gpr_t;
+                for (int q = threadIdx.x; q < groups; q += kBlock) {
+                    const int r = q / gpr_t;
+                    const int cg = q - r * gpr_t;
+                    // band-local output row: in_row0 is a multiple of 16, so local input row
+                    // in_r0 + (r << o) maps to local output row (in_r0 >> o) + r.
+                    const int Rl = (in_r0 >> o) + r;
+                    const int C = (in_c0 >> o) + 4 * cg;
+                    if (Rl < og.rows && C < og.cols) build_group<LT, NT>(g, in, out, taps, b, o, og, Rl, C);
+                }
+            }
+        } else {
+            const long long t = (u - tiles_total) * kBlock + threadIdx.x;
+            const long long per = g->tail_groups_per_img;
+            if (t >= per * g->batch) continue;
+            const int b = (int)(t / per);
+            const long long rem = t - (long long)b * per + g->oct[F].grp_begin;
+            int o = F;
+            while (o + 1 < g->O && rem >= g->oct[o + 1].grp_begin) ++o;
+            const OctGeom og = g->oct[o];
+            const long long k = rem - og.grp_begin;
+            const int Rl = (int)(k / og.gpr);
+            const int C = 4 * (int)(k - (long long)Rl * og.gpr);
+            build_group<LT, NT>(g, in, out, taps, b, o, og, Rl, C);
+        }
+    }
+}
+
+// In-place passes over octaves [o_begin, o_end) of every image (GaussPyInit refill, GaussFilter,
+// DoG, GenerateDoG re-entry).  MODE bits: 1 = window multiply (GaussFilter), 2 = DoG subtract,
+// 4 = refill from the input (GaussPyInit; exclusive).
+template <int LT, int MODE>
+__global__ void __launch_bounds__(kBlock) k_inplace(const Geom* __restrict__ g, const int* __restrict__ in,
+                                                    float* __restrict__ out, const float* __restrict__ taps,
+                                                    int o_begin, int o_end) {
+    const int L = LT > 0 ? LT : g->L;
+    const long long first = g->oct[o_begin].grp_begin;
+    const long long per = (o_end < g->O ? g->oct[o_end].grp_begin
+                                        : g->oct[g->O - 1].grp_begin +
+                                              (long long)g->oct[g->O - 1].rows * g->oct[g->O - 1].gpr) -
+                          first;
+    const long long total = per * g->batch;
+    for (long long t = (long long)blockIdx.x * kBlock + threadIdx.x; t < total; t += (long long)gridDim.x * kBlock) {
+        const int b = (int)(t / per);
+        const long long rem = t - (long long)b * per + first;
+        int o = o_begin;
+        while (o + 1 < o_end && rem >= g->oct[o + 1].grp_begin) ++o;
+        const OctGeom og = g->oct[o];
+        const long long k = rem - og.grp_begin;
+        const int Rl = (int)(k / og.gpr);
+        const int C = 4 * (int)(k - (long long)Rl * og.gpr);
+        const int n = min(4, og.cols - C);
+        const bool full = (n == 4) && ((og.cols & 3) == 0);
+        float* p = out + (long long)b * g->pyr_stride + og.lev_off + (long long)Rl * og.cols + C;
+        auto ld = [&](int s) -> f4 {
+            const float* q = p + s * og.lev_stride;
+            if (full) return ld_f4(q);
+            f4 v = {q[0], 0.f, 0.f, 0.f};
+            if (n > 1) v.y = q[1];
+            if (n > 2) v.z = q[2];
+            if (n > 3) v.w = q[3];
+            return v;
+        };
+        auto st = [&](int s, f4 v) { st_part(p + s * og.lev_stride, v, n, full); };
+        if constexpr (MODE == 4) {
+            const f4 x = load_px(g, in, b, o, og.row0 + Rl, C, n);
+#pragma unroll
+            for (int s = 0; s < L; ++s) st(s, x);
+        } else {
+            const int Rg = og.row0 + Rl;
+            const float* ct = taps + og.ctap + C;
+            const float* rt = taps + og.rtap + Rg;
+            auto win = [&](int s, f4 v) -> f4 {
+                if constexpr ((MODE & 1) != 0) return (v * ld_f4(ct + s * og.ctap_stride)) * rt[s * og.rtap_stride];
+                return v;
+            };
+            if constexpr (MODE == 1) {
+#pragma unroll
+                for (int s = 0; s < L; ++s) st(s, win(s, ld(s)));
+            } else {
+                f4 gp = win(0, ld(0));
+#pragma unroll
+                for (int s = 0; s + 1 < L; ++s) {
+                    const f4 gn = win(s + 1, ld(s + 1));
+                    st(s, gp - gn);
+                    gp = gn;
+                }
+                if constexpr ((MODE & 1) != 0) st(L - 1, gp);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned mix32(unsigned x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// Counter-hash synthetic images, generated in place on each GPU.
+__global__ void __launch_bounds__(kBlock) k_synth(const Geom* __restrict__ g, int* __restrict__ in, unsigned seed,
+                                                  long long first_image) {
+    const long long W = g->W;
+    const long long per = (long long)g->in_rows * W;
+    const long long total = per * g->batch;
+    for (long long t = (long long)blockIdx.x * kBlock + threadIdx.x; t < total; t += (long long)gridDim.x * kBlock) {
+        const long long b = t / per;
+        const long long rem = t - b * per;
+        const long long r = rem / W;
+        const long long c = rem - r * W;
+        const unsigned long long idx =
+            ((unsigned long long)(first_image + b) * (unsigned long long)g->H + (unsigned long long)(g->in_row0 + r)) *
+                (unsigned long long)W +
+            (unsigned long long)c;
+        in[b * g->in_img_stride + r * g->in_pitch + c] = (int)(mix32(seed ^ (unsigned)(idx ^ (idx >> 32))) >> 24);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+// GuassDePyramid.h:7-8 (PI is 3.1414926f in the reference, reproduced on purpose).
+const float kSigma = 2.0f;
+const float kPI = 3.1414926f;
+
+// GuassDePyramid.h:107-121, evaluated on the host in the reference's float expression order:
+// the window centre is the FLOAT length halved o times, minus 1, over 2 (:107-115).
+int host_taps(int length, int octave, int scale, float* out) {
+    float len = (float)length;
+    for (int t = octave; t != 0; --t) len /= 2;
+    const int my_len = (int)len;
+    len = (len - 1) / 2;
+    const float sig = kSigma / (scale + 1);
+    for (int i = 0; i < my_len; ++i) out[i] = expf(-(i - len) * (i - len) / (2 * sig * sig)) / (sig * sqrtf(2 * kPI));
+    return my_len;
+}
+
+int octaves_for(int n) {
+    int x = 0;
+    while (n > 0) {
+        ++x;
+        n /= 2;
+    }
+    return x;
+}
+
+long long round_up(long long v, long long a) { return (v + a - 1) / a * a; }
+
+thread_local std::string g_create_error;
+
+}  // namespace
+
+struct gdp_ctx {
+    int device = 0;
+    Geom geom{};
+    Geom* d_geom = nullptr;
+    int* d_in_own = nullptr;      // context-owned input buffer
+    const int* d_in = nullptr;    // buffer the kernels read (own or caller's)
+    float* d_out = nullptr;
+    float* d_taps = nullptr;
+    std::vector<float> h_taps;
+    long long in_pitch_own = 0, in_img_stride_own = 0;
+    hipStream_t stream = nullptr;
+    int blocks_max = 2048;        // 256 CUs x 8 blocks of 256 threads
+    std::string err;
+    int status(int code, const char* fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }
+};
+
+namespace {
+
+#define GDP_HIP(ctx, call)                                                                                   \
+    do {                                                                                                     \
+        hipError_t e_ = (call);                                                                              \
+        if (e_ != hipSuccess) return (ctx)->status(GDP_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_));    \
+    } while (0)
+
+int upload_geom(gdp_ctx* c) {
+    GDP_HIP(c, hipMemcpy(c->d_geom, &c->geom, sizeof(Geom), hipMemcpyHostToDevice));
+    return GDP_OK;
+}
+
+int launch_build(gdp_ctx* c, hipStream_t st) {
+    const Geom& g = c->geom;
+    const long long units = g.tiles_total + g.tail_units;
+    if (units == 0) return GDP_OK;
+    const int grid = (int)std::min<long long>(units, c->blocks_max);
+    if (g.L == 5)
+        hipLaunchKernelGGL((k_build<5, true>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
+                           c->d_taps);
+    else
+        hipLaunchKernelGGL((k_build<0, true>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
+                           c->d_taps);
+    GDP_HIP(c, hipGetLastError());
+    return GDP_OK;
+}
+
+template <int MODE>
+int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
+    const Geom& g = c->geom;
+    const long long end = oe < g.O ? g.oct[oe].grp_begin
+                                   : g.oct[g.O - 1].grp_begin + (long long)g.oct[g.O - 1].rows * g.oct[g.O - 1].gpr;
+    const long long total = (end - g.oct[ob].grp_begin) * g.batch;
+    if (total <= 0) return GDP_OK;
+    const int grid = (int)std::min<long long>((total + kBlock - 1) / kBlock, c->blocks_max);
+    if (g.L == 5)
+        hipLaunchKernelGGL((k_inplace<5, MODE>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
+                           c->d_taps, ob, oe);
+    else
+        hipLaunchKernelGGL((k_inplace<0, MODE>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
+                           c->d_taps, ob, oe);
+    GDP_HIP(c, hipGetLastError());
+    return GDP_OK;
+}
+
+bool valid_level(const gdp_ctx* c, int b, int o, int s) {
+    return c && b >= 0 && b < c->geom.batch && o >= 0 && o < c->geom.O && s >= 0 && s < c->geom.L;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C ABI
+// ==========================================================================================
+extern "C" {
+
+int gdp_abi_version(void) { return GDP_ABI_VERSION; }
+
+int gdp_octaves_for(int n) { return octaves_for(n); }
+
+const char* gdp_status_string(int s) {
+    switch (s) {
+        case GDP_OK: return "ok";
+        case GDP_ERR_ARG: return "invalid argument";
+        case GDP_ERR_HIP: return "HIP runtime error";
+        case GDP_ERR_STATE: return "invalid state";
+        case GDP_ERR_NOMEM: return "out of memory";
+        case GDP_ERR_NODEV: return "no gfx950 device";
+        default: return "unknown status";
+    }
+}
+
+const char* gdp_last_error(const gdp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int row_begin, int row_end, int device) {
+    if (!out) return GDP_ERR_ARG;
+    *out = nullptr;
+    auto fail = [](int code, const std::string& m) {
+        g_create_error = m;
+        return code;
+    };
+    if (H <= 0 || W <= 0 || S < 0 || S > 60 || batch <= 0 || O < 0)
+        return fail(GDP_ERR_ARG, "gdp_create: need H, W, batch > 0, 0 <= S <= 60, octaves >= 0");
+    const int Omax = octaves_for(std::min(H, W));
+    if (O == 0) O = Omax;
+    if (O > Omax || O > kMaxOct - 1)
+        return fail(GDP_ERR_ARG, "gdp_create: octaves " + std::to_string(O) + " > floor(log2(min(H,W)))+1 = " +
+                                     std::to_string(Omax));
+    const int align = 1 << (std::max(O, kFused) - 1);
+    if (row_begin < 0 || row_end > H || row_begin >= row_end || row_begin % align != 0 ||
+        (row_end != H && row_end % align != 0))
+        return fail(GDP_ERR_ARG, "gdp_create_band: rows [" + std::to_string(row_begin) + ", " +
+                                     std::to_string(row_end) + ") must be multiples of " + std::to_string(align));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GDP_ERR_NODEV, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(GDP_ERR_ARG, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail(GDP_ERR_NODEV, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(GDP_ERR_NODEV, std::string("libgdp is built for gfx950, device is ") + prop.gcnArchName);
+
+    gdp_ctx* c = new (std::nothrow) gdp_ctx();
+    if (!c) return fail(GDP_ERR_NOMEM, "host allocation failed");
+    c->device = device;
+    c->blocks_max = std::max(1, prop.multiProcessorCount) * 8;
+    Geom& g = c->geom;
+    g.H = H;
+    g.W = W;
+    g.S = S;
+    g.L = S + 3;
+    g.O = O;
+    g.F = std::min(O, kFused);
+    g.batch = batch;
+    g.in_row0 = row_begin;
+    g.in_rows = row_end - row_begin;
+    g.in_pitch = round_up(W, 4);
+    g.in_img_stride = (long long)g.in_rows * g.in_pitch;
+    g.vec_in = 1;
+    c->in_pitch_own = g.in_pitch;
+    c->in_img_stride_own = g.in_img_stride;
+
+    // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
+    long long tap_off = 0, lev_off = 0, grp = 0;
+    for (int o = 0; o < O; ++o) {
+        OctGeom& og = g.oct[o];
+        const int Hg = H >> o;
+        og.row0 = (row_begin + (1 << o) - 1) >> o;
+        const int row_hi = (row_end == H) ? Hg : std::min(Hg, (row_end + (1 << o) - 1) >> o);
+        og.rows = std::max(0, row_hi - og.row0);
+        og.cols = W >> o;
+        og.gpr = (og.cols + 3) / 4;
+        og.lev_stride = round_up((long long)og.rows * og.cols, kLevelAlign);
+        og.lev_off = lev_off;
+        lev_off += og.lev_stride * g.L;
+        og.ctap_stride = (int)round_up(og.cols, 4);
+        og.ctap = (int)tap_off;
+        tap_off += (long long)og.ctap_stride * g.L;
+        og.rtap_stride = (int)round_up(Hg, 4);
+        og.rtap = (int)tap_off;
+        tap_off += (long long)og.rtap_stride * g.L;
+        og.grp_begin = grp;
+        grp += (long long)og.rows * og.gpr;
+    }
+    g.pyr_stride = round_up(lev_off, kLevelAlign);
+    g.tiles_r = (g.in_rows + kTileRows - 1) / kTileRows;
+    g.tiles_c = (W + kTileCols - 1) / kTileCols;
+    g.tiles_per_img = (long long)g.tiles_r * g.tiles_c;
+    g.tiles_total = g.tiles_per_img * batch;
+    g.tail_groups_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
+    g.tail_units = (g.tail_groups_per_img * batch + kBlock - 1) / kBlock;
+    if (tap_off > (1ll << 31)) {
+        delete c;
+        return fail(GDP_ERR_ARG, "image too large for the tap table");
+    }
+    c->h_taps.assign((size_t)tap_off, 0.0f);
+    for (int o = 0; o < O; ++o) {
+        const OctGeom& og = g.oct[o];
+        for (int s = 0; s < g.L; ++s) {
+            host_taps(W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride);
+            host_taps(H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride);
+        }
+    }
+
+    auto hip_fail = [&](hipError_t e, const char* what) {
+        std::string m = std::string(what) + ": " + hipGetErrorString(e);
+        gdp_destroy(c);
+        return fail(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, m);
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    if ((e = hipMalloc(&c->d_geom, sizeof(Geom))) != hipSuccess) return hip_fail(e, "hipMalloc(geom)");
+    if ((e = hipMalloc(&c->d_taps, std::max<size_t>(4, c->h_taps.size() * 4))) != hipSuccess)
+        return hip_fail(e, "hipMalloc(taps)");
+    if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)
+        return hip_fail(e, "hipMalloc(input)");
+    if ((e = hipMalloc(&c->d_out, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
+        return hip_fail(e, "hipMalloc(pyramid)");
+    c->d_in = c->d_in_own;
+    if ((e = hipMemcpy(c->d_taps, c->h_taps.data(), c->h_taps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy(taps)");
+    if ((e = hipMemset(c->d_in_own, 0, (size_t)g.in_img_stride * batch * 4)) != hipSuccess) return hip_fail(e, "hipMemset");
+    if (upload_geom(c) != GDP_OK) {
+        std::string m = c->err;
+        gdp_destroy(c);
+        return fail(GDP_ERR_HIP, m);
+    }
+    *out = c;
+    return GDP_OK;
+}
+
+int gdp_create(gdp_ctx** out, int H, int W, int S, int O, int batch, int device) {
+    return gdp_create_band(out, H, W, S, O, batch, 0, H, device);
+}
+
+void gdp_destroy(gdp_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_geom) (void)hipFree(c->d_geom);
+    if (c->d_taps) (void)hipFree(c->d_taps);
+    if (c->d_in_own) (void)hipFree(c->d_in_own);
+    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int gdp_get_geometry(const gdp_ctx* c, int* H, int* W, int* S, int* O, int* batch) {
+    if (!c) return GDP_ERR_ARG;
+    if (H) *H = c->geom.H;
+    if (W) *W = c->geom.W;
+    if (S) *S = c->geom.S;
+    if (O) *O = c->geom.O;
+    if (batch) *batch = c->geom.batch;
+    return GDP_OK;
+}
+
+int gdp_level_dims(const gdp_ctx* c, int o, int* rows, int* cols, int* first_row) {
+    if (!c || o < 0 || o >= c->geom.O) return GDP_ERR_ARG;
+    if (rows) *rows = c->geom.oct[o].rows;
+    if (cols) *cols = c->geom.oct[o].cols;
+    if (first_row) *first_row = c->geom.oct[o].row0;
+    return GDP_OK;
+}
+
+size_t gdp_pyramid_bytes(const gdp_ctx* c) { return c ? (size_t)c->geom.pyr_stride * c->geom.batch * 4 : 0; }
+
+size_t gdp_packed_floats(const gdp_ctx* c) {
+    if (!c) return 0;
+    size_t n = 0;
+    for (int o = 0; o < c->geom.O; ++o) n += (size_t)c->geom.L * c->geom.oct[o].rows * c->geom.oct[o].cols;
+    return n;
+}
+
+int gdp_set_input_host(gdp_ctx* c, int b, const int32_t* base, size_t pitch, void* stream) {
+    if (!c || !base || b < 0 || b >= c->geom.batch || pitch < (size_t)c->geom.W)
+        return c ? c->status(GDP_ERR_ARG, "gdp_set_input_host: bad argument") : GDP_ERR_ARG;
+    if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
+    GDP_HIP(c, hipSetDevice(c->device));
+    hipStream_t st = c->pick(stream);
+    GDP_HIP(c, hipMemcpy2DAsync(c->d_in_own + (size_t)b * c->geom.in_img_stride, (size_t)c->geom.in_pitch * 4, base,
+                                pitch * 4, (size_t)c->geom.W * 4, (size_t)c->geom.in_rows, hipMemcpyHostToDevice, st));
+    GDP_HIP(c, hipStreamSynchronize(st));
+    return GDP_OK;
+}
+
+int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stream) {
+    if (!c || !rows || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_set_input_rows: bad argument") : GDP_ERR_ARG;
+    if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
+    // Gather the row pointers into one pinned staging image, then one 2-D copy.
+    const size_t W = (size_t)c->geom.W, R = (size_t)c->geom.in_rows;
+    std::vector<int32_t> stage(W * R);
+    for (size_t r = 0; r < R; ++r) {
+        if (!rows[r]) return c->status(GDP_ERR_ARG, "gdp_set_input_rows: null row %zu", r);
+        std::memcpy(stage.data() + r * W, rows[r], W * 4);
+    }
+    return gdp_set_input_host(c, b, stage.data(), W, stream);
+}
+
+int gdp_set_input_device(gdp_ctx* c, const int32_t* base, size_t pitch, size_t image_stride) {
+    if (!c) return GDP_ERR_ARG;
+    Geom& g = c->geom;
+    if (!base) {
+        c->d_in = c->d_in_own;
+        g.in_pitch = c->in_pitch_own;
+        g.in_img_stride = c->in_img_stride_own;
+        g.vec_in = 1;
+        return upload_geom(c);
+    }
+    if (pitch < (size_t)g.W || (g.batch > 1 && image_stride < pitch * (size_t)g.in_rows))
+        return c->status(GDP_ERR_ARG, "gdp_set_input_device: pitch/image_stride too small");
+    c->d_in = base;
+    g.in_pitch = (long long)pitch;
+    g.in_img_stride = (long long)image_stride;
+    g.vec_in = ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && pitch % 4 == 0 && image_stride % 4 == 0) ? 1 : 0;
+    return upload_geom(c);
+}
+
+int gdp_fill_synthetic(gdp_ctx* c, uint32_t seed, long first_image, void* stream) {
+    if (!c) return GDP_ERR_ARG;
+    if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
+    GDP_HIP(c, hipSetDevice(c->device));
+    const long long total = (long long)c->geom.in_rows * c->geom.W * c->geom.batch;
+    const int grid = (int)std::min<long long>((total + kBlock - 1) / kBlock, c->blocks_max);
+    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(kBlock), 0, c->pick(stream), c->d_geom, c->d_in_own, seed,
+                       (long long)first_image);
+    GDP_HIP(c, hipGetLastError());
+    return GDP_OK;
+}
+
+int gdp_build(gdp_ctx* c, void* stream) {
+    if (!c) return GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_build(c, c->pick(stream));
+}
+
+int gdp_init(gdp_ctx* c, void* stream) {
+    if (!c) return GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<4>(c, 0, c->geom.O, c->pick(stream));
+}
+
+int gdp_gauss_octave(gdp_ctx* c, int o, void* stream) {
+    if (!c || o < 0 || o >= c->geom.O) return c ? c->status(GDP_ERR_ARG, "octave out of range") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<1>(c, o, o + 1, c->pick(stream));
+}
+
+int gdp_dog_octave(gdp_ctx* c, int o, void* stream) {
+    if (!c || o < 0 || o >= c->geom.O) return c ? c->status(GDP_ERR_ARG, "octave out of range") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<2>(c, o, o + 1, c->pick(stream));
+}
+
+int gdp_generate_dog(gdp_ctx* c, void* stream) {
+    if (!c) return GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<3>(c, 0, c->geom.O, c->pick(stream));
+}
+
+const float* gdp_device_level(const gdp_ctx* c, int b, int o, int s) {
+    if (!valid_level(c, b, o, s)) return nullptr;
+    const OctGeom& og = c->geom.oct[o];
+    return c->d_out + (size_t)b * c->geom.pyr_stride + og.lev_off + (size_t)s * og.lev_stride;
+}
+
+int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) {
+    if (!valid_level(c, b, o, s) || !host) return c ? c->status(GDP_ERR_ARG, "gdp_download_level: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    const OctGeom& og = c->geom.oct[o];
+    GDP_HIP(c, hipMemcpyAsync(host, gdp_device_level(c, b, o, s), (size_t)og.rows * og.cols * 4, hipMemcpyDeviceToHost,
+                              c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+}
+
+int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows) {
+    if (!valid_level(c, b, o, s) || !rows) return c ? c->status(GDP_ERR_ARG, "gdp_download_level_rows: bad argument") : GDP_ERR_ARG;
+    const OctGeom& og = c->geom.oct[o];
+    std::vector<float> tmp((size_t)og.rows * og.cols);
+    int rc = gdp_download_level(c, b, o, s, tmp.data());
+    if (rc != GDP_OK) return rc;
+    for (int r = 0; r < og.rows; ++r) std::memcpy(rows[r], tmp.data() + (size_t)r * og.cols, (size_t)og.cols * 4);
+    return GDP_OK;
+}
+
+int gdp_download_pyramid(gdp_ctx* c, int b, float* host) {
+    if (!c || !host || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    size_t off = 0;
+    for (int o = 0; o < c->geom.O; ++o) {
+        const OctGeom& og = c->geom.oct[o];
+        const size_t n = (size_t)og.rows * og.cols;
+        for (int s = 0; s < c->geom.L; ++s, off += n)
+            if (n) GDP_HIP(c, hipMemcpyAsync(host + off, gdp_device_level(c, b, o, s), n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+}
+
+int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) {
+    if (!c || !host || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_upload_pyramid: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    size_t off = 0;
+    for (int o = 0; o < c->geom.O; ++o) {
+        const OctGeom& og = c->geom.oct[o];
+        const size_t n = (size_t)og.rows * og.cols;
+        for (int s = 0; s < c->geom.L; ++s, off += n)
+            if (n)
+                GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), host + off, n * 4,
+                                          hipMemcpyHostToDevice, c->stream));
+    }
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+}
+
+int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) {
+    if (!c || !host || o < 0 || o >= c->geom.O || s < 0 || s >= c->geom.L || (axis != 0 && axis != 1))
+        return c ? c->status(GDP_ERR_ARG, "gdp_get_taps: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    const OctGeom& og = c->geom.oct[o];
+    const int n = axis == 0 ? og.cols : (c->geom.H >> o);
+    const long long off = axis == 0 ? og.ctap + (long long)s * og.ctap_stride : og.rtap + (long long)s * og.rtap_stride;
+    // read back what the device holds, not the host copy: this is what the kernels use
+    GDP_HIP(c, hipMemcpy(host, c->d_taps + off, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return GDP_OK;
+}
+
+int gdp_sync(gdp_ctx* c) {
+    if (!c) return GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+}
+
+void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int gdp_time_builds(gdp_ctx* c, int iters, void* stream, float* total_ms) {
+    if (!c || iters <= 0 || !total_ms) return c ? c->status(GDP_ERR_ARG, "gdp_time_builds: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    hipStream_t st = c->pick(stream);
+    hipEvent_t e0, e1;
+    GDP_HIP(c, hipEventCreate(&e0));
+    GDP_HIP(c, hipEventCreate(&e1));
+    int rc = GDP_OK;
+    if (hipEventRecord(e0, st) != hipSuccess) rc = c->status(GDP_ERR_HIP, "hipEventRecord");
+    for (int i = 0; i < iters && rc == GDP_OK; ++i) rc = launch_build(c, st);
+    if (rc == GDP_OK && hipEventRecord(e1, st) != hipSuccess) rc = c->status(GDP_ERR_HIP, "hipEventRecord");
+    if (rc == GDP_OK && hipEventSynchronize(e1) != hipSuccess) rc = c->status(GDP_ERR_HIP, "hipEventSynchronize");
+    if (rc == GDP_OK && hipEventElapsedTime(total_ms, e0, e1) != hipSuccess) rc = c->status(GDP_ERR_HIP, "hipEventElapsedTime");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
+}  // extern "C"

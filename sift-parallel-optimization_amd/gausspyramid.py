@@ -1,0 +1,294 @@
+"""Host-side mirror of the reference's pyramid interface, on top of the libgdp C ABI.
+
+`GaussPyramid` keeps the reference class's names, argument meaning and call semantics
+(GuassDePyramid.h:11-29):
+
+    g = GaussPyramid(img, len, S)   # ctor copies img[0:len][0:len] and runs GaussPyInit (:36-58)
+    g.GaussPyInit()                 # refill every level with the decimated input (:60-87)
+    g.GaussFilter(o)                # window-multiply every scale of octave o in place (:106-134)
+    g.GenerateDoG()                 # GaussFilter + DoG for every octave, in place (:136-149)
+    g.output()                      # print scale 0 of every octave (:89-104)
+    g.GaussPy[o][s][r][c]           # the pyramid (downloaded lazily from the device)
+
+Calling GenerateDoG() twice without GaussPyInit() re-filters the pyramid exactly like the
+reference's timing loop does (main.cpp:66-73).  The one behavioural difference is error
+handling: the reference never reports errors (all methods return void); here a failing call
+raises GdpError instead of continuing on bad state.
+
+`PyramidContext` is the batched, stream-ordered interface (one context = `batch` images or one
+row band), used by bench.py and the multi-GPU driver.
+"""
+import ctypes
+import sys
+
+import numpy as np
+
+from ._lib import check, lib
+
+_i = ctypes.c_int
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _stream_handle(stream):
+    """Accept None, an int handle, or a torch.cuda.Stream; return a void* for the C ABI."""
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    handle = getattr(stream, "cuda_stream", None)
+    if handle is not None:
+        return ctypes.c_void_p(handle)
+    raise TypeError(f"unsupported stream object {stream!r}")
+
+
+def octaves_for(n):
+    """floor(log2 n) + 1 — the reference's `layer` (GuassDePyramid.h:48-53)."""
+    return lib().gdp_octaves_for(int(n))
+
+
+class PyramidContext:
+    """`batch` images of H x W int32 (or the row band [row_begin, row_end)) on one GPU.
+
+    Level (o, s) of image b is a rows_o x cols_o float32 array; rows_o covers the band's rows.
+    All compute calls are asynchronous on `stream` (None = the context's own stream).
+    """
+
+    def __init__(self, height, width, S=2, octaves=0, batch=1, device=0, row_begin=0, row_end=None):
+        L = lib()
+        self._ctx = ctypes.c_void_p()
+        row_end = height if row_end is None else row_end
+        check(L.gdp_create_band(ctypes.byref(self._ctx), int(height), int(width), int(S), int(octaves), int(batch),
+                                int(row_begin), int(row_end), int(device)))
+        H, W, S_, O, B = (_i() for _ in range(5))
+        check(L.gdp_get_geometry(self._ctx, *(ctypes.byref(v) for v in (H, W, S_, O, B))), self._ctx)
+        self.H, self.W, self.S, self.O, self.batch = H.value, W.value, S_.value, O.value, B.value
+        self.device = device
+        self.row_begin, self.row_end = int(row_begin), int(row_end)
+        self._dims = []
+        for o in range(self.O):
+            r, c, f = _i(), _i(), _i()
+            check(L.gdp_level_dims(self._ctx, o, ctypes.byref(r), ctypes.byref(c), ctypes.byref(f)), self._ctx)
+            self._dims.append((r.value, c.value, f.value))
+        self._bound = None  # keeps a caller's device input alive
+
+    # ------------------------------------------------------------------ geometry
+    @property
+    def levels_per_octave(self):
+        return self.S + 3
+
+    def level_dims(self, o):
+        """(rows held, cols, first global row) of octave o."""
+        return self._dims[o]
+
+    def packed_floats(self):
+        return lib().gdp_packed_floats(self._ctx)
+
+    def pyramid_bytes(self):
+        return lib().gdp_pyramid_bytes(self._ctx)
+
+    # ------------------------------------------------------------------ input
+    def set_input(self, img, b=0, stream=None):
+        """Upload one H x W (band: band-rows x W) int32 image from host memory."""
+        img = np.ascontiguousarray(img, dtype=np.int32)
+        rows = self.row_end - self.row_begin
+        if img.ndim != 2 or img.shape[1] != self.W or img.shape[0] != rows:
+            raise ValueError(f"expected a ({rows}, {self.W}) image, got {img.shape}")
+        check(lib().gdp_set_input_host(self._ctx, int(b), _ptr(img), self.W, _stream_handle(stream)), self._ctx)
+
+    def set_input_rows(self, rows, b=0, stream=None):
+        """Upload from a list of row arrays — the reference ctor's `int** img` (GuassDePyramid.h:38-46)."""
+        arrs = [np.ascontiguousarray(r, dtype=np.int32) for r in rows]
+        ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        check(lib().gdp_set_input_rows(self._ctx, int(b), ptrs, _stream_handle(stream)), self._ctx)
+
+    def bind_device_input(self, ptr, pitch, image_stride, keepalive=None):
+        """Read images straight from caller device memory (int32 elements for pitch/stride)."""
+        check(lib().gdp_set_input_device(self._ctx, ctypes.c_void_p(ptr), int(pitch), int(image_stride)), self._ctx)
+        self._bound = keepalive
+
+    def unbind_device_input(self):
+        check(lib().gdp_set_input_device(self._ctx, None, 0, 0), self._ctx)
+        self._bound = None
+
+    def fill_synthetic(self, seed=0x5EED, first_image=0, stream=None):
+        check(lib().gdp_fill_synthetic(self._ctx, int(seed) & 0xFFFFFFFF, int(first_image), _stream_handle(stream)),
+              self._ctx)
+
+    # ------------------------------------------------------------------ compute
+    def build(self, stream=None):
+        """Fused GaussPyInit + GenerateDoG of every image (one launch)."""
+        check(lib().gdp_build(self._ctx, _stream_handle(stream)), self._ctx)
+
+    def init(self, stream=None):
+        check(lib().gdp_init(self._ctx, _stream_handle(stream)), self._ctx)
+
+    def gauss_octave(self, o, stream=None):
+        check(lib().gdp_gauss_octave(self._ctx, int(o), _stream_handle(stream)), self._ctx)
+
+    def dog_octave(self, o, stream=None):
+        check(lib().gdp_dog_octave(self._ctx, int(o), _stream_handle(stream)), self._ctx)
+
+    def generate_dog(self, stream=None):
+        check(lib().gdp_generate_dog(self._ctx, _stream_handle(stream)), self._ctx)
+
+    def sync(self):
+        check(lib().gdp_sync(self._ctx), self._ctx)
+
+    @property
+    def stream(self):
+        return lib().gdp_stream(self._ctx)
+
+    def time_builds(self, iters, stream=None):
+        """Total ms of `iters` back-to-back builds, HIP events on the launch stream."""
+        ms = ctypes.c_float()
+        check(lib().gdp_time_builds(self._ctx, int(iters), _stream_handle(stream), ctypes.byref(ms)), self._ctx)
+        return ms.value
+
+    # ------------------------------------------------------------------ output
+    def level(self, b, o, s):
+        rows, cols, _ = self._dims[o]
+        out = np.empty((rows, cols), np.float32)
+        if out.size:
+            check(lib().gdp_download_level(self._ctx, int(b), int(o), int(s), _ptr(out)), self._ctx)
+        return out
+
+    def level_rows(self, b, o, s, rows_out):
+        """Download into a list of preallocated float32 row arrays (float**** materialisation)."""
+        ptrs = (ctypes.c_void_p * len(rows_out))(*[r.ctypes.data for r in rows_out])
+        check(lib().gdp_download_level_rows(self._ctx, int(b), int(o), int(s), ptrs), self._ctx)
+
+    def pyramid(self, b=0):
+        """Packed [o][s][rows][cols] float32 copy of image b's pyramid."""
+        out = np.empty(self.packed_floats(), np.float32)
+        check(lib().gdp_download_pyramid(self._ctx, int(b), _ptr(out)), self._ctx)
+        return out
+
+    def upload_pyramid(self, packed, b=0):
+        packed = np.ascontiguousarray(packed, dtype=np.float32)
+        if packed.size != self.packed_floats():
+            raise ValueError("packed pyramid has the wrong size")
+        check(lib().gdp_upload_pyramid(self._ctx, int(b), _ptr(packed)), self._ctx)
+
+    def levels(self, b=0):
+        """{(o, s): 2-D array} of image b."""
+        return {(o, s): self.level(b, o, s) for o in range(self.O) for s in range(self.S + 3)}
+
+    def device_level_ptr(self, b, o, s):
+        return lib().gdp_device_level(self._ctx, int(b), int(o), int(s))
+
+    def taps(self, axis, o, s):
+        """Window the device holds: axis 0 = column taps (from W), 1 = row taps (from H)."""
+        n = (self.W >> o) if axis == 0 else (self.H >> o)
+        out = np.empty(n, np.float32)
+        check(lib().gdp_get_taps(self._ctx, int(axis), int(o), int(s), _ptr(out)), self._ctx)
+        return out
+
+    # ------------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            lib().gdp_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _LevelView:
+    """GaussPy[o] -> list of S+3 level arrays, downloaded on first access after a change."""
+
+    def __init__(self, owner, o):
+        self._owner, self._o = owner, o
+
+    def __getitem__(self, s):
+        return self._owner._level(self._o, s)
+
+    def __len__(self):
+        return self._owner.S + 3
+
+
+class GaussPyramid:
+    """GPU mirror of `class GaussPyramid` (GuassDePyramid.h:11-29); see the module docstring."""
+
+    def __init__(self, img=None, len=None, S=2, device=0):  # noqa: A002  (reference argument name)
+        # GaussPyramid() (GuassDePyramid.h:31-34): empty object
+        self.data = None
+        self.initialized = False
+        if img is None:
+            return
+        length = int(len)
+        # :38-46 deep copy of img[0:len][0:len] (img may be larger, as in main.cpp:27-35,61)
+        self.data = np.array([np.asarray(img[i][:length], dtype=np.int32) for i in range(length)], dtype=np.int32)
+        self.length = length
+        self.S = int(S)
+        self.layer = octaves_for(length)  # :48-53
+        self._ctx = PyramidContext(length, length, self.S, self.layer, batch=1, device=device)
+        self._ctx.set_input(self.data)
+        self._cache = {}
+        self._fresh = False
+        self.GaussPyInit()  # :57
+
+    # reference surface -------------------------------------------------------
+    def GaussPyInit(self):
+        """:60-87 — refill every level of every octave with the decimated input."""
+        self._ctx.init()
+        self.initialized = True
+        self._fresh = True  # contents == init, so GenerateDoG may take the fused path
+        self._cache.clear()
+
+    def GaussFilter(self, theLayer):
+        """:106-134 — multiply every scale of octave `theLayer` by its window, in place."""
+        self._ctx.gauss_octave(int(theLayer))
+        self._fresh = False
+        self._cache.clear()
+
+    def GenerateDoG(self):
+        """:136-149 — GaussFilter + DoG for every octave, in place on the current contents."""
+        if self._fresh:
+            self._ctx.build()  # fused init+filter+DoG: bit-identical to the in-place sequence
+        else:
+            self._ctx.generate_dog()
+        self._fresh = False
+        self._cache.clear()
+
+    def output(self, file=None):
+        """:89-104 — print scale 0 of each octave (space separated) and an `==` separator row."""
+        file = sys.stdout if file is None else file
+        n = self.length
+        for o in range(self.layer):
+            lev = self._level(o, 0)
+            for row in lev:
+                file.write("".join(f"{v:g} " for v in row) + "\n")
+            file.write("==" * n + "\n")
+            n //= 2
+
+    @property
+    def GaussPy(self):
+        return [_LevelView(self, o) for o in range(self.layer)]
+
+    # helpers -----------------------------------------------------------------
+    def _level(self, o, s):
+        key = (o, s)
+        if key not in self._cache:
+            self._ctx.sync()
+            self._cache[key] = self._ctx.level(0, o, s)
+        return self._cache[key]
+
+    def pyramid(self):
+        """Packed [o][s][r][c] float32 copy (the oracle's layout)."""
+        return self._ctx.pyramid(0)
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None:
+            self._ctx.close()

@@ -1,0 +1,42 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+import __graft_entry__ as entry  # noqa: E402
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """The CPU checker (oracle/) — test infrastructure only."""
+    mod = entry.load_oracle()
+    mod.lib()  # builds liboracle.so on first use if needed
+    return mod
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    """The product package; on a GPU box the HIP library MUST load (no fallback)."""
+    return entry.load_package()
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    import numpy as np
+
+    gdir = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(gdir, "hashes.json")) as f:
+        hashes = json.load(f)
+    dumps = dict(np.load(os.path.join(gdir, "dumps.npz"), allow_pickle=False))
+    taps = dict(np.load(os.path.join(gdir, "taps.npz"), allow_pickle=False))
+    return {"hashes": hashes, "dumps": dumps, "taps": taps}

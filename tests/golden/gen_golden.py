@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors in tests/golden/ from the REFERENCE ITSELF.
+
+The reference (ZhangShuui/SIFT-parallel-optimization) ships no tests, fixtures or golden
+vectors.  Every expected value here is therefore produced by the reference's own
+`GuassDePyramid.h` (and, for the CPU-baseline semantics, `GaussDePyramid-AVX512xOpenMP.h` /
+`-AVX512xPTHREAD.h`), compiled in place by `make -C oracle ref` into oracle/_ref/.  This script
+only runs that binary and stores its outputs as data; it needs /root/reference to exist
+(this container), never the GPU box, which only reads the committed fixtures.
+
+Outputs (all plain data, loadable without pickle):
+  hashes.json   per-level FNV hashes (oracle/gdp_oracle.c:gdo_fnv) of GenerateDoG() output
+  dumps.npz     complete packed pyramids for small n, GenerateDoG re-entry results,
+                the AVX512xOpenMP subset output, and centre windows for n = 512 / 4096
+  taps.npz      the reference's `filter` taps for every (octave, scale) — read from the
+                reference object itself (TapProbe in oracle/ref_harness.cpp)
+  meta.json     generator provenance (glibc, g++, input definitions)
+
+Usage:  make -C oracle ref && python tests/golden/gen_golden.py
+"""
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SERIAL = os.path.join(REPO, "oracle", "_ref", "ref_serial")
+REF_AVX512 = os.path.join(REPO, "oracle", "_ref", "ref_avx512")
+
+# (n, S, input) cases hashed over EVERY octave the reference builds (floor(log2 n)+1).
+HASH_CASES = [
+    (1, 2, "lcg:12345"), (2, 2, "lcg:12345"), (3, 2, "lcg:12345"), (7, 2, "lcg:12345"),
+    (16, 2, "lcg:12345"), (64, 2, "lcg:12345"), (64, 0, "lcg:12345"), (64, 1, "lcg:12345"),
+    (64, 5, "lcg:12345"), (100, 2, "lcg:12345"), (256, 3, "lcg:12345"), (512, 2, "lcg:12345"),
+    (512, 2, "ones"), (513, 3, "lcg:12345"), (1000, 2, "lcg:12345"), (1024, 2, "lcg:777"),
+    (4096, 2, "lcg:12345"),
+    # the benchmark's own input (bench.py / SURVEY.md §8d counter hash), image 0 and 1
+    (4096, 2, "synth:0x5EED:0"), (4096, 2, "synth:0x5EED:1"),
+    (8192, 2, "synth:0x5EED:0"),
+]
+# complete pyramids (every octave, every level) — small enough to commit
+DUMP_CASES = [(1, 2, "lcg:12345"), (2, 2, "lcg:12345"), (3, 2, "lcg:12345"), (7, 2, "lcg:12345"),
+              (16, 2, "lcg:12345"), (64, 2, "lcg:12345"), (64, 3, "lcg:99"), (100, 2, "lcg:12345")]
+# GenerateDoG() called repeatedly without GaussPyInit (main.cpp:66-73 timing loop semantics)
+REGEN_CASES = [(64, 2, "lcg:12345", 2), (64, 2, "lcg:12345", 3), (37, 1, "lcg:5", 2)]
+# AVX512xOpenMP::GenerateDoG_nomp_dynamic output (subset semantics) and AVX512xPTHREAD output
+SUBSET_CASES = [(64, 2, "lcg:12345"), (256, 2, "lcg:12345")]
+WINDOW_CASES = [(512, 2, "lcg:12345"), (4096, 2, "lcg:12345")]
+WINDOW = 96
+TAP_CASES = [(512, 2), (100, 2), (1000, 2), (513, 3), (4096, 2), (1080, 2), (1920, 2), (37, 1)]
+
+
+def octaves_of(n):
+    x = 0
+    while n:
+        x += 1
+        n //= 2
+    return x
+
+
+def level_slices(n, S):
+    """(o, s) -> slice of the packed float32 layout of oracle/ref_harness.cpp:dump()."""
+    out, off = {}, 0
+    for o in range(octaves_of(n)):
+        m = n >> o
+        for s in range(S + 3):
+            out[(o, s)] = (off, m)
+            off += m * m
+    return out, off
+
+
+def run(*args):
+    return subprocess.run(list(args), check=True, capture_output=True, text=True).stdout
+
+
+def dump(binary, mode, n, S, inp, *extra):
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "out.f32")
+        run(binary, mode, str(n), str(S), inp, *extra, path)
+        return np.fromfile(path, dtype=np.float32)
+
+
+def key(*parts):
+    return "_".join(str(p).replace(":", "-") for p in parts)
+
+
+def main():
+    for b in (REF_SERIAL, REF_AVX512):
+        if not os.path.exists(b):
+            sys.exit(f"missing {b}: run `make -C oracle ref` first")
+    hashes = []
+    for n, S, inp in HASH_CASES:
+        rec = json.loads(run(REF_SERIAL, "hash", str(n), str(S), inp))
+        rec["input"] = inp
+        hashes.append(rec)
+        print("hash", n, S, inp, flush=True)
+
+    arrays = {}
+    for n, S, inp in DUMP_CASES:
+        arrays[key("full", n, S, inp)] = dump(REF_SERIAL, "dump", n, S, inp)
+    for n, S, inp, calls in REGEN_CASES:
+        arrays[key("regen", n, S, inp, calls)] = dump(REF_SERIAL, "regen", n, S, inp, str(calls))
+    for n, S, inp in SUBSET_CASES:
+        arrays[key("a512omp", n, S, inp)] = dump(REF_AVX512, "dump-a512omp", n, S, inp)
+        full = dump(REF_AVX512, "dump-a512xp", n, S, inp)
+        ser = dump(REF_SERIAL, "dump", n, S, inp)
+        # recorded as a fact about the reference, checked again by tests/test_oracle.py
+        arrays[key("a512xp_equals_serial", n, S, inp)] = np.array([np.array_equal(full.view(np.uint32), ser.view(np.uint32))])
+    for n, S, inp in WINDOW_CASES:
+        pyr = dump(REF_SERIAL, "dump", n, S, inp)
+        sl, _ = level_slices(n, S)
+        for o in range(4):
+            m = n >> o
+            h = min(WINDOW, m)
+            r0 = m // 2 - h // 2
+            for s in range(S + 3):
+                off, _ = sl[(o, s)]
+                lev = pyr[off:off + m * m].reshape(m, m)
+                arrays[key("win", n, S, inp, o, s)] = lev[r0:r0 + h, r0:r0 + h].copy()
+        arrays[key("winorigin", n, S, inp)] = np.array([m // 2 - min(WINDOW, m) // 2 for m in (n >> o for o in range(4))])
+        print("window", n, flush=True)
+    np.savez_compressed(os.path.join(HERE, "dumps.npz"), **arrays)
+
+    taps = {}
+    with tempfile.TemporaryDirectory() as td:
+        for n, S in TAP_CASES:
+            path = os.path.join(td, "t.f32")
+            run(REF_SERIAL, "taps", str(n), str(S), path)
+            t = np.fromfile(path, dtype=np.float32)
+            off = 0
+            for s in range(S + 3):
+                for o in range(octaves_of(n)):
+                    m = n >> o
+                    taps[key("taps", n, S, o, s)] = t[off:off + m]
+                    off += m
+            assert off == t.size
+    np.savez_compressed(os.path.join(HERE, "taps.npz"), **taps)
+
+    with open(os.path.join(HERE, "hashes.json"), "w") as f:
+        json.dump(hashes, f, indent=1)
+    gxx = run("g++", "--version").splitlines()[0]
+    meta = {
+        "generator": "tests/golden/gen_golden.py via oracle/_ref/ref_serial + ref_avx512 "
+                     "(reference headers compiled in place by oracle/Makefile)",
+        "reference_files": ["GuassDePyramid.h", "GaussDePyramid-AVX512xOpenMP.h", "GaussDePyramid-AVX512xPTHREAD.h"],
+        "glibc": platform.libc_ver()[1], "gxx": gxx,
+        "hash": "h0=0xcbf29ce484222325; h=(h^bits32)*0x100000001b3 mod 2^64 over float32 bits, row-major per level",
+        "inputs": {
+            "lcg:SEED": "s=SEED; per pixel row-major: s=s*1664525+1013904223 mod 2^32; px=s>>24",
+            "ones": "every pixel 1 (main.cpp:31-35)",
+            "synth:SEED:B": "idx=(B*n+r)*n+c (u64); x=SEED^(u32)(idx^(idx>>32)); lowbias32(x)>>24",
+        },
+        "layout": "packed: levels in (octave, scale) order, each (n>>o)x(n>>o) row-major float32",
+        "window": f"centre window of {WINDOW}x{WINDOW} (or the whole level), origin listed in winorigin_*",
+    }
+    with open(os.path.join(HERE, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

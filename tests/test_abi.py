@@ -1,0 +1,88 @@
+"""The C-ABI boundary on a machine without a GPU: the library builds, loads, exports exactly what
+include/gdp.h declares, and the host-only callers (C++ drop-in header, example driver) compile.
+No compute call is made here."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "sift-parallel-optimization_amd")
+
+
+def test_library_built_and_loads(pkg):
+    assert os.path.exists(os.path.join(PKG, "lib", "libgdp.so"))
+    assert pkg.lib().gdp_abi_version() == 1
+
+
+def test_every_header_function_is_exported(pkg):
+    declared = pkg.header_functions()
+    assert len(declared) >= 25
+    L = pkg.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(PKG, "lib", "libgdp.so")], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line and line.split()[-1].startswith("gdp_")}
+    assert exported == set(declared), exported ^ set(declared)
+
+
+def test_python_signatures_cover_header(pkg):
+    from sift_parallel_optimization_amd._lib import SIGNATURES
+
+    assert set(SIGNATURES) == set(pkg.header_functions())
+
+
+def test_host_only_entry_points(pkg):
+    L = pkg.lib()
+    for n, want in [(1, 1), (2, 2), (512, 10), (513, 10), (4096, 13), (0, 0)]:
+        assert L.gdp_octaves_for(n) == want
+    assert L.gdp_status_string(0) == b"ok"
+    assert L.gdp_status_string(5) == b"no gfx950 device"
+    assert L.gdp_device_level(None, 0, 0, 0) is None
+    assert L.gdp_packed_floats(None) == 0
+
+
+def test_create_rejects_bad_arguments(pkg):
+    L = pkg.lib()
+    ctx = ctypes.c_void_p()
+    for args in [(0, 16, 2, 0, 1, 0), (16, 16, -1, 0, 1, 0), (16, 16, 2, 6, 1, 0), (16, 16, 2, 0, 0, 0)]:
+        assert L.gdp_create(ctypes.byref(ctx), *args) == 1, args
+        assert ctx.value is None
+    # band rows must be aligned to 2^(max(O,5)-1)
+    assert L.gdp_create_band(ctypes.byref(ctx), 64, 64, 2, 5, 1, 8, 64, 0) == 1
+    assert b"multiples of 16" in L.gdp_last_error(None)
+
+
+def test_create_without_gpu_fails_loudly(pkg):
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    with pytest.raises(pkg.GdpError):
+        pkg.PyramidContext(64, 64, 2)
+
+
+def test_cpp_dropin_header_compiles_with_plain_gxx(tmp_path):
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "GaussDePyramid-HIP.h"\nint main(){ GaussPyramid_hip g; (void)g; return 0; }\n')
+    subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Werror", "-I" + os.path.join(REPO, "include"),
+                    str(src)], check=True)
+
+
+def test_example_driver_links():
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
+    assert os.path.exists(os.path.join(REPO, "examples", "main_hip"))
+
+
+def test_product_never_reaches_the_oracle():
+    """No source under the package may load oracle/ (no CPU fallback on the product path)."""
+    for root, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                text = open(os.path.join(root, f)).read()
+                assert "liboracle" not in text and "gdp_oracle" not in text and "load_oracle" not in text, f

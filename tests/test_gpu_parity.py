@@ -1,0 +1,315 @@
+"""Parity of the HIP path (through the C ABI) with the reference — bit-exact, 0 ULP.
+
+Expected values: tests/golden/ (the reference's own outputs) and the oracle (oracle/, pinned to
+those same fixtures by tests/test_oracle.py).  Tolerance: none — every float32 word must be
+identical, including the sign of zero and every subnormal (bit-exact is the bar,
+the ≤2-ULP fallback is not needed and not used).  Runs on an MI355X: pytest -m gpu.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _assert_same(got, want, what):
+    g, w = _bits(got), _bits(want)
+    assert g.shape == w.shape, (what, g.shape, w.shape)
+    bad = np.flatnonzero(g.ravel() != w.ravel())
+    assert bad.size == 0, f"{what}: {bad.size} words differ, first at {bad[:5]}"
+
+
+def _gpu_pyramid(pkg, img, S, O=0, **kw):
+    H, W = img.shape
+    with pkg.PyramidContext(H, W, S=S, octaves=O, batch=1, **kw) as ctx:
+        ctx.set_input(img)
+        ctx.build()
+        ctx.sync()
+        return ctx.pyramid(0)
+
+
+# ------------------------------------------------------------------ taps
+def test_device_taps_are_the_reference_taps(pkg, golden):
+    """Host-computed (glibc expf) taps uploaded to the device == reference `filter` bits."""
+    cases = {}
+    for name in golden["taps"]:
+        _, n, S, o, s = name.split("_")
+        cases.setdefault((int(n), int(S)), []).append((int(o), int(s), name))
+    for (n, S), items in cases.items():
+        with pkg.PyramidContext(n, n, S=S) as ctx:
+            for o, s, name in items:
+                _assert_same(ctx.taps(0, o, s), golden["taps"][name], f"col taps {name}")
+                _assert_same(ctx.taps(1, o, s), golden["taps"][name], f"row taps {name}")
+    # non-square: columns use the W-derived window, rows the H-derived one
+    with pkg.PyramidContext(1080, 1920, S=2) as ctx:
+        for o in range(ctx.O):
+            for s in range(5):
+                _assert_same(ctx.taps(0, o, s), golden["taps"][f"taps_1920_2_{o}_{s}"], ("1920", o, s))
+                _assert_same(ctx.taps(1, o, s), golden["taps"][f"taps_1080_2_{o}_{s}"], ("1080", o, s))
+
+
+# ------------------------------------------------------------------ full builds vs reference
+def test_build_matches_reference_level_hashes(pkg, oracle, golden):
+    """Every octave / scale / element of 20 reference runs, incl. non-power-of-two n (float-halved
+    window centre), S in {0,1,2,3,5}, all-ones input, and the bench input at 4096^2 and 8192^2."""
+    for rec in golden["hashes"]:
+        n, S, spec = rec["n"], rec["S"], rec["input"]
+        with pkg.PyramidContext(n, n, S=S) as ctx:
+            if spec.startswith("synth:"):  # device-side generator: also pins gdp_fill_synthetic
+                _, seed, idx = spec.split(":")
+                ctx.fill_synthetic(int(seed, 0), int(idx, 0))
+            else:
+                ctx.set_input(oracle.image_from_spec(n, spec))
+            ctx.build()
+            ctx.sync()
+            assert ctx.O == len(rec["octaves"])
+            for o, row in enumerate(rec["octaves"]):
+                for s, h in enumerate(row):
+                    assert oracle.fnv(ctx.level(0, o, s)) == int(h, 16), (n, S, spec, o, s)
+
+
+def test_build_matches_reference_dumps(pkg, oracle, golden):
+    for name, arr in golden["dumps"].items():
+        if not name.startswith("full_"):
+            continue
+        _, n, S, spec = name.split("_", 3)
+        got = _gpu_pyramid(pkg, oracle.image_from_spec(int(n), spec.replace("-", ":")), int(S))
+        _assert_same(got, arr, name)
+
+
+def test_centre_windows(pkg, oracle, golden):
+    n, S, spec = 4096, 2, "lcg:12345"
+    with pkg.PyramidContext(n, n, S=S, octaves=4) as ctx:
+        ctx.set_input(oracle.image_from_spec(n, spec))
+        ctx.build()
+        origins = golden["dumps"]["winorigin_4096_2_lcg-12345"]
+        for o in range(4):
+            for s in range(5):
+                win = golden["dumps"][f"win_4096_2_lcg-12345_{o}_{s}"]
+                r0 = int(origins[o])
+                lev = ctx.level(0, o, s)
+                _assert_same(lev[r0:r0 + win.shape[0], r0:r0 + win.shape[1]], win, (o, s))
+
+
+@pytest.mark.parametrize("H,W,S,O", [
+    (1, 1, 2, 0), (2, 3, 2, 0), (5, 7, 1, 0), (17, 33, 2, 0), (37, 53, 3, 0), (64, 64, 0, 0),
+    (100, 31, 2, 0), (129, 255, 5, 0), (255, 129, 2, 4), (256, 256, 7, 0), (300, 500, 2, 5),
+    (1080, 1920, 2, 5), (1080, 1920, 2, 0), (513, 513, 3, 0), (1024, 4, 2, 0), (4, 1024, 2, 0),
+    (777, 1001, 2, 6), (2048, 2048, 2, 12),
+])
+def test_build_matches_oracle_shapes(pkg, oracle, H, W, S, O):
+    """Ragged/odd/tiny/non-square shapes, every S path (templated S=2 and generic), octave limits."""
+    img = oracle.lcg_image(H, W, 1000 + H * 7 + W)
+    want = oracle.build_pyramid(img, S, O or None)
+    _assert_same(_gpu_pyramid(pkg, img, S, O), want, (H, W, S, O))
+
+
+def test_large_value_and_negative_inputs(pkg, oracle):
+    """int32 beyond 2^24 (float rounding of the conversion) and negative pixels (-0.0 products)."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(-2**31, 2**31 - 1, size=(64, 96), dtype=np.int64).astype(np.int32)
+    img[::7] = -1
+    img[:, ::5] = 0
+    _assert_same(_gpu_pyramid(pkg, img, 2), oracle.build_pyramid(img, 2), "wide-range ints")
+
+
+# ------------------------------------------------------------------ batch / band / device input
+def test_batched_build(pkg, oracle):
+    H, W, B = 120, 200, 5
+    imgs = [oracle.lcg_image(H, W, 50 + b) for b in range(B)]
+    with pkg.PyramidContext(H, W, S=2, batch=B) as ctx:
+        for b, img in enumerate(imgs):
+            ctx.set_input(img, b)
+        ctx.build()
+        for b, img in enumerate(imgs):
+            _assert_same(ctx.pyramid(b), oracle.build_pyramid(img, 2), ("batch", b))
+
+
+def test_synthetic_batch_matches_oracle_generator(pkg, oracle):
+    H, W, B, first = 64, 96, 3, 17
+    with pkg.PyramidContext(H, W, S=2, batch=B) as ctx:
+        ctx.fill_synthetic(0x5EED, first)
+        ctx.build()
+        for b in range(B):
+            want = oracle.build_pyramid(oracle.synthetic_image(H, W, 0x5EED, first + b), 2)
+            _assert_same(ctx.pyramid(b), want, ("synthetic", b))
+
+
+@pytest.mark.parametrize("H,W,O,bands", [(1024, 768, 5, [0, 256, 512, 768, 1024]), (700, 300, 5, [0, 16, 400, 700]),
+                                         (1024, 1024, 7, [0, 64, 512, 1024])])
+def test_row_bands_reassemble_the_image(pkg, oracle, H, W, O, bands):
+    """Row-band contexts (multi-GPU config 5 partition): halo 0, bands tile every level exactly."""
+    img = oracle.lcg_image(H, W, 3)
+    want = oracle.levels(oracle.build_pyramid(img, 2, O), H, W, 2, O)
+    got = {k: np.zeros_like(v) for k, v in want.items()}
+    for r0, r1 in zip(bands[:-1], bands[1:]):
+        with pkg.PyramidContext(H, W, S=2, octaves=O, row_begin=r0, row_end=r1) as ctx:
+            ctx.set_input(img[r0:r1])
+            ctx.build()
+            for o in range(O):
+                rows, cols, first = ctx.level_dims(o)
+                for s in range(5):
+                    got[(o, s)][first:first + rows] = ctx.level(0, o, s)
+    for k in want:
+        _assert_same(got[k], want[k], ("band", k))
+
+
+def test_device_input_binding(pkg, oracle):
+    """Zero-copy input from caller device memory: aligned (int4 loads) and unaligned pitch paths."""
+    import torch
+
+    for H, W, pitch in [(96, 128, 128), (96, 128, 131), (50, 37, 37)]:
+        imgs = [oracle.lcg_image(H, W, 9 + b) for b in range(2)]
+        host = np.zeros((2, H, pitch), np.int32)
+        for b in range(2):
+            host[b, :, :W] = imgs[b]
+        dev = torch.from_numpy(host).cuda()
+        with pkg.PyramidContext(H, W, S=2, batch=2) as ctx:
+            ctx.bind_device_input(dev.data_ptr(), pitch, H * pitch, keepalive=dev)
+            ctx.build(torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            for b in range(2):
+                _assert_same(ctx.pyramid(b), oracle.build_pyramid(imgs[b], 2), ("devin", H, W, pitch, b))
+            ctx.unbind_device_input()
+
+
+def test_int_star_star_upload(pkg, oracle):
+    img = oracle.lcg_image(40, 40, 1)
+    with pkg.PyramidContext(40, 40, S=2) as ctx:
+        ctx.set_input_rows([img[r] for r in range(40)])
+        ctx.build()
+        _assert_same(ctx.pyramid(0), oracle.build_pyramid(img, 2), "int** upload")
+
+
+# ------------------------------------------------------------------ in-place ops / re-entry
+def test_inplace_ops_match_reference_order(pkg, oracle):
+    H, W, S = 72, 104, 2
+    O = oracle.default_octaves(H, W)
+    img = oracle.lcg_image(H, W, 21)
+    with pkg.PyramidContext(H, W, S=S) as ctx:
+        ctx.set_input(img)
+        ctx.init()
+        want = oracle.init_pyramid(img, S)
+        _assert_same(ctx.pyramid(0), want, "GaussPyInit")
+        for o in range(O):
+            ctx.gauss_octave(o)
+            oracle.gauss_octave(want, H, W, S, o)
+            _assert_same(ctx.pyramid(0), want, ("GaussFilter", o))
+            ctx.dog_octave(o)
+            oracle.dog_octave(want, H, W, S, o)
+            _assert_same(ctx.pyramid(0), want, ("DoG", o))
+        ctx.generate_dog()  # re-entry on already-filtered contents
+        oracle.generate_dog(want, H, W, S, O)
+        _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
+
+
+def test_generate_dog_reentry_vs_reference(pkg, oracle, golden):
+    for name, arr in golden["dumps"].items():
+        if not name.startswith("regen_"):
+            continue
+        _, n, S, spec, calls = name.split("_")
+        g = pkg.GaussPyramid(oracle.image_from_spec(int(n), spec.replace("-", ":")), int(n), int(S))
+        for _ in range(int(calls)):
+            g.GenerateDoG()
+        _assert_same(g.pyramid(), arr, name)
+        g.close()
+
+
+def test_gausspyramid_mirror_surface(pkg, oracle, golden, capsys):
+    """The reference-named class: ctor on a larger int** image, GaussPy indexing, output()."""
+    big = oracle.lcg_image(80, 80, 12345)
+    n = 64
+    img = oracle.lcg_image(n, n, 12345)
+    big[:n, :n] = img
+    g = pkg.GaussPyramid([list(r) for r in big], n, 2)
+    assert g.initialized and g.layer == 7
+    assert float(g.GaussPy[0][3][5][6]) == float(img[5, 6])  # after GaussPyInit: decimated input
+    g.GenerateDoG()
+    full = golden["dumps"]["full_64_2_lcg-12345"]
+    _assert_same(g.pyramid(), full, "mirror GenerateDoG")
+    lv = oracle.levels(full, n, n, 2, 7)
+    assert float(g.GaussPy[2][1][7][9]) == float(lv[(2, 1)][7, 9])
+    g.output()
+    text = capsys.readouterr().out.splitlines()
+    assert text[0] == "".join(f"{v:g} " for v in lv[(0, 0)][0])
+    assert text[n] == "==" * n
+    g.GaussFilter(1)
+    oracle.gauss_octave(full := full.copy(), n, n, 2, 1)
+    _assert_same(g.pyramid(), full, "mirror GaussFilter")
+    g.close()
+
+
+def test_errors_are_loud(pkg):
+    with pkg.PyramidContext(32, 32, S=2) as ctx:
+        with pytest.raises(pkg.GdpError):
+            ctx.gauss_octave(99)
+        with pytest.raises(pkg.GdpError):
+            ctx.level(5, 0, 0)
+    with pytest.raises(pkg.GdpError):
+        pkg.PyramidContext(32, 32, S=2, octaves=9)
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_config3_batch_1080p(pkg, oracle):
+    """64 x 1080x1920, 5 octaves (BASELINE config 3) — a spread of images checked exactly."""
+    with pkg.PyramidContext(1080, 1920, S=2, octaves=5, batch=64) as ctx:
+        ctx.fill_synthetic(0x5EED, 0)
+        ctx.build()
+        for b in (0, 1, 31, 63):
+            want = oracle.build_pyramid(oracle.synthetic_image(1080, 1920, 0x5EED, b), 2, 5)
+            _assert_same(ctx.pyramid(b), want, ("c3", b))
+
+
+def test_config5_16384_bands_equal_whole_image(pkg, oracle):
+    """16384^2, 5 octaves: 8 row bands (config 5 partition) == one whole-image build, and the
+    whole-image octave 4 / a centre slab of octave 0 == the oracle."""
+    n, O = 16384, 5
+    with pkg.PyramidContext(n, n, S=2, octaves=O) as full:
+        full.fill_synthetic(0x5EED, 0)
+        full.build()
+        full.sync()
+        per = n // 8
+        for k in (0, 3, 7):
+            with pkg.PyramidContext(n, n, S=2, octaves=O, row_begin=k * per, row_end=(k + 1) * per) as band:
+                band.fill_synthetic(0x5EED, 0)
+                band.build()
+                for o in range(O):
+                    rows, cols, first = band.level_dims(o)
+                    for s in (0, 4):
+                        _assert_same(band.level(0, o, s), full.level(0, o, s)[first:first + rows], ("c5", k, o, s))
+        # whole-image values vs the closed form (numpy float32 with the oracle's taps, itself
+        # pinned to the reference by tests/test_oracle.py::test_numpy_restatement_nonsquare)
+        img = oracle.synthetic_image(n, n, 0x5EED, 0)
+        for o, r0, r1 in [(0, 8000, 8256), (4, 0, n >> 4)]:
+            x = img[r0 << o:r1 << o:1 << o, ::1 << o].astype(np.float32)
+            G = [(x * oracle.taps(n, o, s)[None, :]) * oracle.taps(n, o, s)[r0:r1, None] for s in range(5)]
+            for s in range(5):
+                want = G[s] - G[s + 1] if s < 4 else G[s]
+                _assert_same(full.level(0, o, s)[r0:r1], want, ("c5 closed form", o, s))
+
+
+# ------------------------------------------------------------------ C++ drop-in driver
+def test_cpp_dropin_driver_matches_reference(oracle, golden, tmp_path):
+    exe = os.path.join(REPO, "examples", "main_hip")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
+    out = tmp_path / "p.f32"
+    subprocess.run([exe, "512", "2", "lcg:12345", str(out), "1"], check=True, timeout=120)
+    got = np.fromfile(out, dtype=np.float32)
+    rec = [r for r in golden["hashes"] if r["n"] == 512 and r["input"] == "lcg:12345"][0]
+    lv = oracle.levels(got, 512, 512, 2, 10)
+    for o, row in enumerate(rec["octaves"]):
+        for s, h in enumerate(row):
+            assert oracle.fnv(lv[(o, s)]) == int(h, 16), (o, s)
+    subprocess.run([exe, "64", "2", "lcg:12345", str(out), "3"], check=True, timeout=120)
+    _assert_same(np.fromfile(out, dtype=np.float32), golden["dumps"]["regen_64_2_lcg-12345_3"], "driver regen x3")
+    timing = subprocess.run([exe], check=True, timeout=120, capture_output=True, text=True).stdout
+    assert float(timing.strip()) > 0
