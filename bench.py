@@ -186,7 +186,9 @@ def main():
         scaling = "weak"
         units_all = world * B * H * W
     ctx.sync()
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-null) torch stream: the builds and the HIP events share it
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
 
     for _ in range(args.warmup):
         ctx.build(stream)

@@ -136,6 +136,17 @@ size_t gdp_packed_floats(const gdp_ctx* ctx);
  * the reference's own (tests/golden/taps.npz). */
 int gdp_get_taps(gdp_ctx* ctx, int axis, int octave, int scale, float* host);
 
+/* ---- tuning (performance only; results are bit-identical for every setting) --------------- */
+enum {
+    GDP_TUNE_NONTEMPORAL = 1,   /* 1 (default): pyramid stores bypass cache allocation (nt)   */
+    GDP_TUNE_BLOCKS_PER_CU = 2, /* value > 0: persistent build grid = CUs x value;
+                                   0 (default): one 16x256 tile per block                      */
+    GDP_TUNE_GRID = 3,          /* explicit build grid size; 0 (default) = automatic         */
+    GDP_TUNE_VARIANT = 4        /* build kernel code variant (block size / tile width), 0..6;
+                                   default chosen from the image width                         */
+};
+int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
+
 /* ---- misc ---------------------------------------------------------------------------------- */
 int gdp_sync(gdp_ctx* ctx);                    /* wait for the context's stream */
 void* gdp_stream(const gdp_ctx* ctx);          /* the context's own hipStream_t */

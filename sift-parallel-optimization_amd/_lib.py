@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("GDP_LIBRARY", os.path.join(PKG_DIR, "lib", "libgdp.so
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "gdp.h")
 
 GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV = range(6)
+GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT = 1, 2, 3, 4
 
 
 class GdpError(RuntimeError):
@@ -65,6 +66,7 @@ SIGNATURES = {
     "gdp_last_error": (ctypes.c_char_p, [_p]),
     "gdp_status_string": (ctypes.c_char_p, [_c_int]),
     "gdp_time_builds": (_c_int, [_p, _c_int, _p, ctypes.POINTER(ctypes.c_float)]),
+    "gdp_set_tuning": (_c_int, [_p, _c_int, _c_int]),
 }
 
 

@@ -36,10 +36,11 @@ namespace {
 // geometry
 // ------------------------------------------------------------------------------------------
 constexpr int kMaxOct = 32;
-constexpr int kBlock = 256;     // 4 waves
+constexpr int kBlock = 256;     // 4 waves (in-place / synthetic kernels)
+constexpr int kTailGroups = 256; // groups of 4 pixels per tail work unit
 constexpr int kFused = 5;       // octaves 0..4 share one 16 x 256 input tile
 constexpr int kTileRows = 16;   // 2^(kFused-1): every fused octave has whole rows in a tile
-constexpr int kTileCols = 256;  // octave 0: one wave = one tile row = 64 lanes x 4 pixels
+constexpr int kTileCols = 256;  // tile width of the register octave-0 path (64 lanes x 4 pixels)
 constexpr int kLevelAlign = 64; // floats (256 B) — every level starts 16-B (and 256-B) aligned
 
 struct OctGeom {
@@ -64,8 +65,8 @@ struct Geom {
     long long in_pitch, in_img_stride;
     long long pyr_stride; // floats between image pyramids
     int tiles_r, tiles_c;
-    long long tiles_per_img, tiles_total;
-    long long tail_groups_per_img, tail_units; // octaves >= F, 256 groups per unit
+    unsigned tiles_per_img, tiles_total;       // host checks the unit count fits 31 bits
+    unsigned tail_groups_per_img, tail_units;  // octaves >= F, 256 groups per unit
     OctGeom oct[kMaxOct];
 };
 
@@ -145,56 +146,155 @@ __device__ __forceinline__ void build_group(const Geom* __restrict__ g, const in
         st_part(dst + (L - 1) * og.lev_stride, gp, n, false);
 }
 
+// Octave 0 of one 16 x 256 tile, S+3 = LT known at compile time: wave w owns tile rows w, w+4,
+// w+8, w+12 and lane l owns columns 4l..4l+3 of each.  The LT column windows of the lane are
+// loaded once into registers and reused for the 4 rows; the row windows are wave-uniform
+// (scalar loads); the 4 int4 input loads are issued before any arithmetic.  Every wave store is
+// 64 lanes x 16 B = 1 KiB contiguous of one level row.
+template <int LT, bool NT>
+__device__ __forceinline__ void tile_octave0(const Geom* __restrict__ g, const int* __restrict__ in,
+                                             float* __restrict__ out, const float* __restrict__ taps, int b,
+                                             int in_r0, int in_c0) {
+    const OctGeom og = g->oct[0];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int C = in_c0 + 4 * lane;
+    if (C >= og.cols) return;
+    const int n = min(4, og.cols - C);
+    const bool full = (n == 4) && ((og.cols & 3) == 0);
+    constexpr int kRows = kTileRows / 4;
+    f4 fc[LT];
+#pragma unroll
+    for (int s = 0; s < LT; ++s) fc[s] = ld_f4(taps + og.ctap + s * og.ctap_stride + C);
+    f4 x[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+        const int Rl = in_r0 + wave + 4 * k;
+        x[k] = Rl < og.rows ? load_px(g, in, b, 0, og.row0 + Rl, C, n) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    float* base = out + (long long)b * g->pyr_stride + og.lev_off + C;
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+        const int Rl = in_r0 + wave + 4 * k; // wave-uniform
+        if (Rl >= og.rows) break;
+        const float* rt = taps + og.rtap + og.row0 + Rl;
+        float* dst = base + (long long)Rl * og.cols;
+        f4 gp = (x[k] * fc[0]) * rt[0];
+#pragma unroll
+        for (int s = 0; s + 1 < LT; ++s) {
+            const f4 gn = (x[k] * fc[s + 1]) * rt[(s + 1) * og.rtap_stride];
+            if (full)
+                st_f4<NT>(dst + s * og.lev_stride, gp - gn);
+            else
+                st_part(dst + s * og.lev_stride, gp - gn, n, false);
+            gp = gn;
+        }
+        if (full)
+            st_f4<NT>(dst + (LT - 1) * og.lev_stride, gp);
+        else
+            st_part(dst + (LT - 1) * og.lev_stride, gp, n, false);
+    }
+}
+
 // Fused build.  Work units: [0, tiles_total) are 16 x 256 input tiles (octaves 0..F-1 of the
 // tile: octave o covers (16>>o) rows x (256>>o) columns, reading lines the o = 0 pass of the
 // same block just brought on chip); [tiles_total, +tail_units) are 256-group slices of the tiny
-// octaves >= F.  Persistent grid-stride loop over units (grid <= 8 blocks per CU).
-template <int LT, bool NT>
-__global__ void __launch_bounds__(kBlock) k_build(const Geom* __restrict__ g, const int* __restrict__ in,
-                                                  float* __restrict__ out, const float* __restrict__ taps) {
-    const long long tiles_total = g->tiles_total;
-    const long long units = tiles_total + g->tail_units;
+// octaves >= F.  Default launch: one unit per block (the dispatcher back-fills CUs as blocks
+// retire, which measured faster than a persistent grid); the grid-stride loop serves capped grids.
+// BLK = threads per block; O0REG selects the register-resident octave-0 path (BLK = 256 only).
+template <int LT, bool NT, int BLK, int TC, bool O0REG>
+__device__ __forceinline__ void build_body(const Geom* __restrict__ g, const int* __restrict__ in,
+                                           float* __restrict__ out, const float* __restrict__ taps) {
+    const unsigned tiles_total = g->tiles_total;
+    const unsigned units = tiles_total + g->tail_units;
     const int F = g->F;
-    for (long long u = blockIdx.x; u < units; u += gridDim.x) {
+    for (unsigned u = blockIdx.x; u < units; u += gridDim.x) {
         if (u < tiles_total) {
-            const int b = (int)(u / g->tiles_per_img);
-            const long long rem = u - (long long)b * g->tiles_per_img;
-            const int tr = (int)(rem / g->tiles_c);
-            const int tc = (int)(rem - (long long)tr * g->tiles_c);
-            const int in_r0 = tr * kTileRows; // band-local input row of the tile
-            const int in_c0 = tc * kTileCols;
+            const unsigned b = u / g->tiles_per_img;
+            const unsigned rem = u - b * g->tiles_per_img;
+            const unsigned tr = rem / (unsigned)g->tiles_c;
+            const unsigned tc = rem - tr * (unsigned)g->tiles_c;
+            const int in_r0 = (int)tr * kTileRows; // band-local input row of the tile
+            const int in_c0 = (int)tc * TC;
 #pragma unroll
             for (int o = 0; o < kFused; ++o) {
                 if (o >= F) break;
+                if constexpr (LT > 0 && O0REG && BLK == 256 && TC == kTileCols) {
+                    if (o == 0) {
+                        tile_octave0<LT, NT>(g, in, out, taps, (int)b, in_r0, in_c0);
+                        continue;
+                    }
+                }
                 const OctGeom og = g->oct[o];
-                const int gpr_t = (kTileCols / 4) >> o; // 64, 32, 16, 8, 4
+                const int gpr_t = (TC / 4) >> o; // groups per tile row (TC = 256: 64, 32, 16, 8, 4)
                 const int groups = (kTileRows >> o) * gpr_t;
-                for (int q = threadIdx.x; q < groups; q += kBlock) {
+#pragma unroll
+                for (int q0 = 0; q0 < groups; q0 += BLK) {
+                    const int q = q0 + (int)threadIdx.x;
+                    if (q >= groups) break;
                     const int r = q / gpr_t;
                     const int cg = q - r * gpr_t;
                     // band-local output row: in_row0 is a multiple of 16, so local input row
                     // in_r0 + (r << o) maps to local output row (in_r0 >> o) + r.
                     const int Rl = (in_r0 >> o) + r;
                     const int C = (in_c0 >> o) + 4 * cg;
-                    if (Rl < og.rows && C < og.cols) build_group<LT, NT>(g, in, out, taps, b, o, og, Rl, C);
+                    if (Rl < og.rows && C < og.cols) build_group<LT, NT>(g, in, out, taps, (int)b, o, og, Rl, C);
                 }
             }
         } else {
-            const long long t = (u - tiles_total) * kBlock + threadIdx.x;
-            const long long per = g->tail_groups_per_img;
-            if (t >= per * g->batch) continue;
-            const int b = (int)(t / per);
-            const long long rem = t - (long long)b * per + g->oct[F].grp_begin;
-            int o = F;
-            while (o + 1 < g->O && rem >= g->oct[o + 1].grp_begin) ++o;
-            const OctGeom og = g->oct[o];
-            const long long k = rem - og.grp_begin;
-            const int Rl = (int)(k / og.gpr);
-            const int C = 4 * (int)(k - (long long)Rl * og.gpr);
-            build_group<LT, NT>(g, in, out, taps, b, o, og, Rl, C);
+            for (int q = threadIdx.x; q < kTailGroups; q += BLK) {
+                const unsigned t = (u - tiles_total) * kTailGroups + q;
+                const unsigned per = g->tail_groups_per_img;
+                if (t >= per * (unsigned)g->batch) break;
+                const unsigned b = t / per;
+                const long long rem = (long long)(t - b * per) + g->oct[F].grp_begin;
+                int o = F;
+                while (o + 1 < g->O && rem >= g->oct[o + 1].grp_begin) ++o;
+                const OctGeom og = g->oct[o];
+                const int k = (int)(rem - og.grp_begin);
+                const int Rl = k / og.gpr;
+                const int C = 4 * (k - Rl * og.gpr);
+                build_group<LT, NT>(g, in, out, taps, (int)b, o, og, Rl, C);
+            }
         }
     }
 }
+
+template <int LT, bool NT, int BLK, int TC, bool O0REG>
+__global__ void __launch_bounds__(BLK) k_build(const Geom* __restrict__ g, const int* __restrict__ in,
+                                               float* __restrict__ out, const float* __restrict__ taps) {
+    build_body<LT, NT, BLK, TC, O0REG>(g, in, out, taps);
+}
+
+// Build-kernel code variants (GDP_TUNE_VARIANT); all bit-identical, A/B'd by tools/tune.py.
+struct BuildVariant {
+    int block, tile_cols;
+    void (*k[2][2])(const Geom*, const int*, float*, const float*); // [LT==5][NT]
+};
+#define GDP_VARIANT(BLK, TC, REG)                                                                \
+    BuildVariant {                                                                               \
+        BLK, TC, {{k_build<0, false, BLK, TC, REG>, k_build<0, true, BLK, TC, REG>},              \
+                  {k_build<5, false, BLK, TC, REG>, k_build<5, true, BLK, TC, REG>}}              \
+    }
+const BuildVariant kVariants[] = {
+    GDP_VARIANT(1024, 256, false), // 0 (default): 16 waves, one octave-0 group per thread
+    GDP_VARIANT(256, 256, true),   // 1: 4 waves, register-resident octave 0 (4 groups per thread)
+    GDP_VARIANT(512, 256, false),  // 2: 8 waves, 2 groups per thread
+    GDP_VARIANT(256, 256, false),  // 3: 4 waves, generic loop
+    GDP_VARIANT(512, 128, false),  // 4: 8 waves, 16 x 128 tile, one group per thread
+    GDP_VARIANT(1024, 512, false), // 5: 16 waves, 16 x 512 tile, 2 groups per thread
+    GDP_VARIANT(256, 64, false),   // 6: 4 waves, 16 x 64 tile, one group per thread
+};
+
+// Default variant for a width (tools/tune.py, MI355X): 1024 threads on 16 x 256 tiles (v0) is the
+// fastest everywhere the width fills its tiles; when a 256-wide tile grid would leave more lanes
+// idle than a 128-wide one (e.g. W = 1920: 7.5 tiles), 512 threads on 16 x 128 tiles (v4).
+int default_variant(int W) {
+    const long long waste256 = (long long)((W + 255) / 256) * 256 - W;
+    const long long waste128 = (long long)((W + 127) / 128) * 128 - W;
+    return waste256 * 128 > waste128 * 256 ? 4 : 0;
+}
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // In-place passes over octaves [o_begin, o_end) of every image (GaussPyInit refill, GaussFilter,
 // DoG, GenerateDoG re-entry).  MODE bits: 1 = window multiply (GaussFilter), 2 = DoG subtract,
@@ -334,7 +434,12 @@ struct gdp_ctx {
     std::vector<float> h_taps;
     long long in_pitch_own = 0, in_img_stride_own = 0;
     hipStream_t stream = nullptr;
+    int cus = 256;
     int blocks_max = 2048;        // 256 CUs x 8 blocks of 256 threads
+    int nontemporal = 1;          // GDP_TUNE_NONTEMPORAL
+    int grid_override = 0;        // GDP_TUNE_GRID (0 = automatic)
+    int persistent = 0;           // set by GDP_TUNE_BLOCKS_PER_CU: grid = CUs x blocks per CU
+    int variant = 0;              // GDP_TUNE_VARIANT: index into kVariants (default_variant(W))
     std::string err;
     int status(int code, const char* fmt, ...) {
         char buf[512];
@@ -356,22 +461,38 @@ namespace {
         if (e_ != hipSuccess) return (ctx)->status(GDP_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_));    \
     } while (0)
 
+// Tile grid of the selected build variant (tile width differs per variant).
+int retile(gdp_ctx* c, int tile_cols) {
+    Geom& g = c->geom;
+    g.tiles_r = (g.in_rows + kTileRows - 1) / kTileRows;
+    g.tiles_c = (g.W + tile_cols - 1) / tile_cols;
+    const long long tiles_per_img = (long long)g.tiles_r * g.tiles_c;
+    if (tiles_per_img * g.batch + g.tail_units >= (1ll << 31))
+        return c->status(GDP_ERR_ARG, "image/batch too large for one context (split the batch)");
+    g.tiles_per_img = (unsigned)tiles_per_img;
+    g.tiles_total = (unsigned)(tiles_per_img * g.batch);
+    return GDP_OK;
+}
+
+// Geometry changes are configuration-time events: drain the device first so no in-flight launch
+// (on any stream) reads a half-updated Geom.
 int upload_geom(gdp_ctx* c) {
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipDeviceSynchronize());
     GDP_HIP(c, hipMemcpy(c->d_geom, &c->geom, sizeof(Geom), hipMemcpyHostToDevice));
     return GDP_OK;
 }
 
 int launch_build(gdp_ctx* c, hipStream_t st) {
     const Geom& g = c->geom;
-    const long long units = g.tiles_total + g.tail_units;
+    const long long units = (long long)g.tiles_total + g.tail_units;
     if (units == 0) return GDP_OK;
-    const int grid = (int)std::min<long long>(units, c->blocks_max);
-    if (g.L == 5)
-        hipLaunchKernelGGL((k_build<5, true>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
-                           c->d_taps);
-    else
-        hipLaunchKernelGGL((k_build<0, true>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
-                           c->d_taps);
+    // default: one unit per block; GDP_TUNE_GRID / GDP_TUNE_BLOCKS_PER_CU cap it (persistent loop)
+    const long long cap = c->grid_override > 0 ? c->grid_override : (c->persistent ? c->blocks_max : units);
+    const int grid = (int)std::min<long long>(units, cap);
+    const BuildVariant& v = kVariants[c->variant];
+    hipLaunchKernelGGL(v.k[g.L == 5][c->nontemporal ? 1 : 0], dim3(grid), dim3(v.block), 0, st, c->d_geom, c->d_in,
+                       c->d_out, c->d_taps);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
 }
@@ -453,7 +574,9 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     gdp_ctx* c = new (std::nothrow) gdp_ctx();
     if (!c) return fail(GDP_ERR_NOMEM, "host allocation failed");
     c->device = device;
-    c->blocks_max = std::max(1, prop.multiProcessorCount) * 8;
+    c->variant = default_variant(W);
+    c->cus = std::max(1, prop.multiProcessorCount);
+    c->blocks_max = c->cus * 8;
     Geom& g = c->geom;
     g.H = H;
     g.W = W;
@@ -493,16 +616,17 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         grp += (long long)og.rows * og.gpr;
     }
     g.pyr_stride = round_up(lev_off, kLevelAlign);
-    g.tiles_r = (g.in_rows + kTileRows - 1) / kTileRows;
-    g.tiles_c = (W + kTileCols - 1) / kTileCols;
-    g.tiles_per_img = (long long)g.tiles_r * g.tiles_c;
-    g.tiles_total = g.tiles_per_img * batch;
-    g.tail_groups_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
-    g.tail_units = (g.tail_groups_per_img * batch + kBlock - 1) / kBlock;
-    if (tap_off > (1ll << 31)) {
+    const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
+    const long long tail_units = (tail_per_img * batch + kTailGroups - 1) / kTailGroups;
+    const long long min_tiles = (long long)((g.in_rows + kTileRows - 1) / kTileRows) * ((W + 63) / 64) * batch;
+    if (tap_off > (1ll << 31) || min_tiles + tail_units >= (1ll << 31) || tail_per_img * batch >= (1ll << 31) ||
+        grp >= (1ll << 31)) {
         delete c;
-        return fail(GDP_ERR_ARG, "image too large for the tap table");
+        return fail(GDP_ERR_ARG, "image/batch too large for one context (split the batch)");
     }
+    g.tail_groups_per_img = (unsigned)tail_per_img;
+    g.tail_units = (unsigned)tail_units;
+    retile(c, kVariants[c->variant].tile_cols);
     c->h_taps.assign((size_t)tap_off, 0.0f);
     for (int o = 0; o < O; ++o) {
         const OctGeom& og = g.oct[o];
@@ -745,6 +869,38 @@ int gdp_sync(gdp_ctx* c) {
 }
 
 void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int gdp_set_tuning(gdp_ctx* c, int key, int value) {
+    if (!c) return GDP_ERR_ARG;
+    switch (key) {
+        case GDP_TUNE_NONTEMPORAL:
+            c->nontemporal = value ? 1 : 0;
+            return GDP_OK;
+        case GDP_TUNE_BLOCKS_PER_CU:
+            if (value < 0 || value > 64) return c->status(GDP_ERR_ARG, "blocks per CU must be in [0, 64]");
+            c->persistent = value > 0;
+            c->blocks_max = c->cus * (value > 0 ? value : 8);
+            return GDP_OK;
+        case GDP_TUNE_GRID:
+            if (value < 0) return c->status(GDP_ERR_ARG, "grid must be >= 0");
+            c->grid_override = value;
+            return GDP_OK;
+        case GDP_TUNE_VARIANT: {
+            if (value < 0 || value >= kNumVariants) return c->status(GDP_ERR_ARG, "variant out of range");
+            const int old = c->variant;
+            c->variant = value;
+            int rc = retile(c, kVariants[value].tile_cols);
+            if (rc == GDP_OK) rc = upload_geom(c);
+            if (rc != GDP_OK) {
+                c->variant = old;
+                retile(c, kVariants[old].tile_cols);
+            }
+            return rc;
+        }
+        default:
+            return c->status(GDP_ERR_ARG, "unknown tuning key %d", key);
+    }
+}
 
 int gdp_time_builds(gdp_ctx* c, int iters, void* stream, float* total_ms) {
     if (!c || iters <= 0 || !total_ms) return c ? c->status(GDP_ERR_ARG, "gdp_time_builds: bad argument") : GDP_ERR_ARG;

@@ -141,6 +141,15 @@ class PyramidContext:
     def stream(self):
         return lib().gdp_stream(self._ctx)
 
+    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None):
+        """Performance knobs of the build kernel (outputs are bit-identical for every setting)."""
+        from ._lib import GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_VARIANT
+
+        for key, val in ((GDP_TUNE_NONTEMPORAL, nontemporal), (GDP_TUNE_BLOCKS_PER_CU, blocks_per_cu),
+                         (GDP_TUNE_GRID, grid), (GDP_TUNE_VARIANT, variant)):
+            if val is not None:
+                check(lib().gdp_set_tuning(self._ctx, key, int(val)), self._ctx)
+
     def time_builds(self, iters, stream=None):
         """Total ms of `iters` back-to-back builds, HIP events on the launch stream."""
         ms = ctypes.c_float()

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of build-kernel tunings in ONE process (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/tune.py [--config c2] [--iters 50] [--rounds 7]
+
+Every variant builds the same resident synthetic batch; each round times every variant once
+(HIP events around `iters` back-to-back launches on the context stream); prints per-variant
+median / min per-launch ms and the algorithmic-byte rate, one JSON line per variant.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+import __graft_entry__ as entry  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
+    args = ap.parse_args()
+    pkg = entry.load_package()
+    cfg = bench.CONFIGS[args.config]
+    H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
+    ctx = pkg.PyramidContext(H, W, S=2, octaves=O, batch=B)
+    ctx.fill_synthetic(bench.SEED, 0)
+    ctx.sync()
+    ref = None
+    variants = []
+    for v in args.variants.split(";"):
+        kv = dict(p.split("=") for p in v.split(","))
+        variants.append((v, {"nontemporal": int(kv.get("nt", 1)), "grid": int(kv.get("grid", "0"), 0),
+                             "variant": int(kv.get("v", 0))}))
+        if "bpc" in kv:
+            variants[-1][1]["blocks_per_cu"] = int(kv["bpc"])
+    times = {name: [] for name, _ in variants}
+
+    def apply(kw):  # fresh context state per variant: persistent only when bpc is given
+        ctx.set_tuning(**{k: v for k, v in kw.items() if k != "blocks_per_cu"})
+        if "blocks_per_cu" in kw:
+            ctx.set_tuning(blocks_per_cu=kw["blocks_per_cu"])
+        else:
+            ctx.set_tuning(blocks_per_cu=0)
+
+    for name, kw in variants:  # warm-up + identical-output check for every variant
+        apply(kw)
+        ctx.build()
+        ctx.sync()
+        lev = ctx.level(0, 0, 0)
+        if ref is None:
+            ref = lev
+        assert np.array_equal(lev.view(np.uint32), ref.view(np.uint32)), name
+    for _ in range(args.rounds):
+        for name, kw in variants:
+            apply(kw)
+            times[name].append(ctx.time_builds(args.iters) / args.iters)
+    nbytes = bench.algorithmic_bytes(H, W, 2, O, B)
+    for name, _ in variants:
+        t = np.array(times[name])
+        print(json.dumps({"variant": name, "config": args.config, "ms_median": round(float(np.median(t)), 5),
+                          "ms_min": round(float(t.min()), 5),
+                          "GBps_median": round(nbytes / (np.median(t) / 1e3) / 1e9, 1)}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
