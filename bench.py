@@ -246,7 +246,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(pmc["kernel_bytes_per_launch"]) if pmc else None,
-            "kernel": "k_build<5,true> (fused decimate+window+DoG)",
+            "kernel": "k_build (fused decimate+window+DoG), variant %d" % ctx.tuning()["variant"],
             "kernel_ms": round(kernel_ms, 6),
             "algorithmic_bytes_per_launch": bytes_launch,
         },

@@ -146,6 +146,7 @@ enum {
                                    default chosen from the image width                         */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
+int gdp_get_tuning(const gdp_ctx* ctx, int key, int* value);
 
 /* ---- misc ---------------------------------------------------------------------------------- */
 int gdp_sync(gdp_ctx* ctx);                    /* wait for the context's stream */

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 runs of bench.py into profiles/ (committed evidence for bench.py's roofline).
+
+Inputs (written on the GPU box under gpurun_out/ by tools/gpu_session.sh steps):
+  <trace>/run_kernel_stats.csv          rocprofv3 --kernel-trace --stats
+  <fetch>/run_counter_collection.csv    rocprofv3 --pmc FETCH_SIZE   (its own pass)
+  <write>/run_counter_collection.csv    rocprofv3 --pmc WRITE_SIZE   (its own pass)
+Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE and WRITE_SIZE
+are KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read,
+so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+
+Writes profiles/pmc_<config>_<round>.json (read by bench.py for roofline.traffic) and copies the
+kernel-stats CSV to profiles/rocprof_<config>_<round>_kernel_stats.csv.
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+KERNEL = "k_build"
+
+
+def counter_values(path, counter):
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--round", default="r01")
+    ap.add_argument("--bench-json", help="bench.py output line of the traced run (optional)")
+    args = ap.parse_args()
+
+    import bench
+
+    stats = None
+    with open(os.path.join(args.trace, "run_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            if KERNEL in r["Name"]:
+                stats = r
+    fetch = counter_values(os.path.join(args.fetch, "run_counter_collection.csv"), "FETCH_SIZE")
+    write = counter_values(os.path.join(args.write, "run_counter_collection.csv"), "WRITE_SIZE")
+    cfg = bench.CONFIGS[args.config]
+    alg = bench.algorithmic_bytes(cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"])
+    read_b = 2 * statistics.median(fetch) * 1024
+    write_b = statistics.median(write) * 1024
+    rec = {
+        "config": args.config, "round": args.round, "kernel": stats["Name"] if stats else KERNEL,
+        "trace_calls": int(stats["Calls"]) if stats else None,
+        "trace_avg_ns": float(stats["AverageNs"]) if stats else None,
+        "trace_min_ns": float(stats["MinNs"]) if stats else None,
+        "fetch_size_kib_median": statistics.median(fetch), "write_size_kib_median": statistics.median(write),
+        "dispatches_counted": [len(fetch), len(write)],
+        "read_bytes_corrected": read_b, "write_bytes": write_b,
+        "kernel_bytes_per_launch": read_b + write_b,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (read_b + write_b) / alg,
+        "trace_GBps_algorithmic": alg / (float(stats["AverageNs"]) * 1e-9) / 1e9 if stats else None,
+        "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads); write = WRITE_SIZE KiB",
+    }
+    if args.bench_json and os.path.exists(args.bench_json):
+        with open(args.bench_json) as f:
+            for line in f:
+                if line.startswith("{"):
+                    rec["bench_line_of_traced_run"] = json.loads(line)
+    out = os.path.join(HERE, f"pmc_{args.config}_{args.round}.json")
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    shutil.copy(os.path.join(args.trace, "run_kernel_stats.csv"),
+                os.path.join(HERE, f"rocprof_{args.config}_{args.round}_kernel_stats.csv"))
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()

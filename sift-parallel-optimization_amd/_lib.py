@@ -67,6 +67,7 @@ SIGNATURES = {
     "gdp_status_string": (ctypes.c_char_p, [_c_int]),
     "gdp_time_builds": (_c_int, [_p, _c_int, _p, ctypes.POINTER(ctypes.c_float)]),
     "gdp_set_tuning": (_c_int, [_p, _c_int, _c_int]),
+    "gdp_get_tuning": (_c_int, [_p, _c_int, ctypes.POINTER(_c_int)]),
 }
 
 

@@ -870,6 +870,17 @@ int gdp_sync(gdp_ctx* c) {
 
 void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
+    if (!c || !value) return GDP_ERR_ARG;
+    switch (key) {
+        case GDP_TUNE_NONTEMPORAL: *value = c->nontemporal; return GDP_OK;
+        case GDP_TUNE_BLOCKS_PER_CU: *value = c->persistent ? c->blocks_max / c->cus : 0; return GDP_OK;
+        case GDP_TUNE_GRID: *value = c->grid_override; return GDP_OK;
+        case GDP_TUNE_VARIANT: *value = c->variant; return GDP_OK;
+        default: return GDP_ERR_ARG;
+    }
+}
+
 int gdp_set_tuning(gdp_ctx* c, int key, int value) {
     if (!c) return GDP_ERR_ARG;
     switch (key) {

@@ -150,6 +150,18 @@ class PyramidContext:
             if val is not None:
                 check(lib().gdp_set_tuning(self._ctx, key, int(val)), self._ctx)
 
+    def tuning(self):
+        """Current {nontemporal, blocks_per_cu, grid, variant} of the build kernel."""
+        from ._lib import GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_VARIANT
+
+        out = {}
+        for name, key in (("nontemporal", GDP_TUNE_NONTEMPORAL), ("blocks_per_cu", GDP_TUNE_BLOCKS_PER_CU),
+                          ("grid", GDP_TUNE_GRID), ("variant", GDP_TUNE_VARIANT)):
+            v = _i()
+            check(lib().gdp_get_tuning(self._ctx, key, ctypes.byref(v)), self._ctx)
+            out[name] = v.value
+        return out
+
     def time_builds(self, iters, stream=None):
         """Total ms of `iters` back-to-back builds, HIP events on the launch stream."""
         ms = ctypes.c_float()

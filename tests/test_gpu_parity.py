@@ -112,6 +112,26 @@ def test_build_matches_oracle_shapes(pkg, oracle, H, W, S, O):
     _assert_same(_gpu_pyramid(pkg, img, S, O), want, (H, W, S, O))
 
 
+@pytest.mark.parametrize("variant", range(7))
+def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
+    """Every code variant of the build kernel (block size / tile width / octave-0 path, also
+    persistent grids and plain stores) produces identical bits."""
+    for H, W, S, O in [(100, 300, 2, 0), (67, 1000, 3, 5), (256, 512, 2, 9), (33, 65, 1, 0)]:
+        img = oracle.lcg_image(H, W, 77 + variant)
+        want = oracle.build_pyramid(img, S, O or None)
+        with pkg.PyramidContext(H, W, S=S, octaves=O) as ctx:
+            ctx.set_input(img)
+            for kw in ({"variant": variant}, {"nontemporal": 0}, {"blocks_per_cu": 1}, {"grid": 3}):
+                ctx.set_tuning(**kw)
+                ctx.build()
+                _assert_same(ctx.pyramid(0), want, (variant, H, W, S, O, kw))
+
+
+def test_default_variant_follows_width(pkg):
+    with pkg.PyramidContext(64, 4096, S=2) as a, pkg.PyramidContext(64, 1920, S=2) as b:
+        assert a.tuning()["variant"] == 0 and b.tuning()["variant"] == 4
+
+
 def test_large_value_and_negative_inputs(pkg, oracle):
     """int32 beyond 2^24 (float rounding of the conversion) and negative pixels (-0.0 products)."""
     rng = np.random.default_rng(5)
