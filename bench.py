@@ -139,6 +139,33 @@ def latest_pmc(config_key):
     return best
 
 
+def verify(ctx, cfg, key, world, rank, dist, mg):
+    """After the timed region: gdp_checksum of what the benchmark built vs the checksum of the
+    reference's own output for the same input (tests/golden/checksums.json).  Image configs check
+    global image 0 (rank 0); the row-band config sums every rank's band checksum."""
+    path = os.path.join(REPO, "tests", "golden", "checksums.json")
+    with open(path) as f:
+        fixtures = {(r["n"], r["input"].lower()): r for r in json.load(f)}
+    H, O = cfg["H"], cfg["O"]
+    rec = fixtures.get((H, f"synth:{SEED:#x}:0".lower())) if cfg["H"] == cfg["W"] else None
+    if cfg["band"]:
+        sums = mg.gather_checksums([ctx.checksum(0)], dist=dist)
+        if rank != 0:
+            return None
+        got = sum(v[0] for v in sums) & 0xFFFFFFFFFFFFFFFF
+        what = f"sum of {world} row-band checksums"
+    else:
+        if rank != 0:
+            return None
+        got = ctx.checksum(0)
+        what = "global image 0"
+    if rec is None or f"octaves_{O}" not in rec:
+        return {"status": "unchecked (no reference fixture for this input)", "checksum": f"{got:016x}"}
+    want = int(rec[f"octaves_{O}"], 16)
+    return {"status": "bit-exact" if got == want else "MISMATCH", "checked": what,
+            "checksum": f"{got:016x}", "reference_checksum": f"{want:016x}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,22 +187,29 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    # one process per GPU; GDP_BENCH_BACKEND=gloo lets a 1-GPU box rehearse N ranks on device 0
+    backend = os.environ.get("GDP_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local if backend == "nccl" else local % max(1, ndev)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["batch"] = args.batch
     H, W, S, O, B = cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"]
+    mg = __import__(pkg.__name__ + ".distributed", fromlist=["plan_band"])
     if cfg["band"]:
-        # one image, row bands aligned to 2^(O-1) rows: each rank owns rows [r0, r1)
-        align = 1 << (max(O, 5) - 1)
-        per = -(-H // world // align) * align
-        r0, r1 = min(H, rank * per), min(H, (rank + 1) * per)
+        # one image, row bands aligned to 2^(max(O,5)-1) rows: each rank owns rows [r0, r1)
+        r0, r1 = mg.plan_band(H, world, rank, O)
         ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=1, device=local, row_begin=r0, row_end=r1)
         ctx.fill_synthetic(SEED, 0)
         scaling = "strong"
@@ -209,10 +243,8 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
-    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall, kernel_ms = float(t[0]), float(t[1])
+    wall, kernel_ms = mg.max_over_ranks([wall, kernel_ms], dist=dist, device=red_dev)
+    parity = verify(ctx, cfg, args.config, world, rank, dist, mg)
 
     # roofline of the (only) kernel of a step, per launch on THIS rank's share
     rows_local = ctx.row_end - ctx.row_begin
@@ -251,6 +283,7 @@ def main():
             "algorithmic_bytes_per_launch": bytes_launch,
         },
     }
+    result["parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
     elif rank == 0:

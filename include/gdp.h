@@ -12,8 +12,8 @@
  *  - Every function returns an int status (GDP_OK == 0) unless documented otherwise; no C++
  *    exception crosses the ABI.  gdp_last_error(ctx) / gdp_status_string() describe failures.
  *  - Only plain pointers and sizes cross the boundary.  `stream` is a hipStream_t passed as
- *    void* (NULL = the context's own stream); all compute and copy calls are stream-ordered and
- *    asynchronous unless documented otherwise.
+ *    void*: NULL = the context's own stream, GDP_STREAM_NULL = HIP's default (null) stream; all
+ *    compute and copy calls are stream-ordered and asynchronous unless documented otherwise.
  *  - The context owns its device buffers (input, pyramid, tap tables); the caller keeps
  *    ownership of every host array it passes in.  One context per host thread and device.
  *  - Semantics are the reference's, bit for bit: float32 taps from glibc expf/sqrtf computed on
@@ -41,6 +41,9 @@ extern "C" {
 #endif
 
 typedef struct gdp_ctx gdp_ctx;
+
+/* Stream argument selecting HIP's default (null) stream; NULL selects the context's stream. */
+#define GDP_STREAM_NULL ((void*)1)
 
 enum {
     GDP_OK = 0,
@@ -129,6 +132,17 @@ int gdp_download_pyramid(gdp_ctx* ctx, int b, float* host);
 int gdp_upload_pyramid(gdp_ctx* ctx, int b, const float* host);
 /* Float elements of one image's packed pyramid (what gdp_download_pyramid writes). */
 size_t gdp_packed_floats(const gdp_ctx* ctx);
+/* Zero-copy output: write the pyramids into caller-owned DEVICE memory of at least
+ * gdp_pyramid_bytes() bytes, 256-B aligned (e.g. a torch tensor that a collective then moves).
+ * Level (o, s) of image b starts gdp_level_offset() floats into it.  base = NULL restores the
+ * context's own buffer. */
+int gdp_set_output_device(gdp_ctx* ctx, float* base, size_t bytes);
+size_t gdp_level_offset(const gdp_ctx* ctx, int b, int octave, int scale);
+/* Order-independent 64-bit checksum of image b's pyramid (blocking): the sum, mod 2^64, over
+ * every word of every level of splitmix64_fin(idx * 0x9E3779B97F4A7C15 + (o*64+s) *
+ * 0xD1B54A32D192ED03 + float_bits), idx = global_row * cols + col.  Row-band checksums add up
+ * to the whole image's, so multi-GPU runs are verified by gathering 8 bytes per rank. */
+int gdp_checksum(gdp_ctx* ctx, int b, uint64_t* out);
 
 /* ---- taps ---------------------------------------------------------------------------------- */
 /* The column (axis = 0, from W) or row (axis = 1, from H) window of (o, s) the context uploaded,

@@ -200,3 +200,35 @@ def ref_dump(mode, n, S, spec, *extra):
         path = os.path.join(td, "o.f32")
         subprocess.run([binary, mode, str(n), str(S), spec, *map(str, extra), path], check=True, capture_output=True)
         return np.fromfile(path, dtype=np.float32)
+
+
+# ---------------------------------------------------------------- checksum (gdp_checksum restated)
+_PHI = np.uint64(0x9E3779B97F4A7C15)
+_LVL = np.uint64(0xD1B54A32D192ED03)
+
+
+def _splitmix_fin(x):
+    x = x ^ (x >> np.uint64(30))
+    x = x * np.uint64(0xBF58476D1CE4E5B9)
+    x = x ^ (x >> np.uint64(27))
+    x = x * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def level_checksum(lev, o, s, first_row=0):
+    """Contribution of one level (rows starting at global row `first_row`) to gdp_checksum."""
+    lev = np.ascontiguousarray(lev, dtype=np.float32)
+    rows, cols = lev.shape
+    with np.errstate(over="ignore"):
+        idx = (np.arange(rows, dtype=np.uint64)[:, None] + np.uint64(first_row)) * np.uint64(cols) + \
+            np.arange(cols, dtype=np.uint64)[None, :]
+        x = idx * _PHI + np.uint64(o * 64 + s) * _LVL + lev.view(np.uint32).astype(np.uint64)
+        return int(_splitmix_fin(x).sum(dtype=np.uint64))
+
+
+def pyramid_checksum(pyr, H, W, S, O):
+    """gdp_checksum of a whole-image packed pyramid."""
+    total = 0
+    for (o, s), lev in levels(pyr, H, W, S, O).items():
+        total = (total + level_checksum(lev, o, s)) & 0xFFFFFFFFFFFFFFFF
+    return total

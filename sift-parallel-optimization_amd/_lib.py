@@ -60,6 +60,9 @@ SIGNATURES = {
     "gdp_download_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_upload_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_packed_floats": (_c_size, [_p]),
+    "gdp_set_output_device": (_c_int, [_p, _p, _c_size]),
+    "gdp_level_offset": (_c_size, [_p, _c_int, _c_int, _c_int]),
+    "gdp_checksum": (_c_int, [_p, _c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "gdp_get_taps": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_sync": (_c_int, [_p]),
     "gdp_stream": (_p, [_p]),

@@ -361,6 +361,46 @@ __global__ void __launch_bounds__(kBlock) k_inplace(const Geom* __restrict__ g, 
     }
 }
 
+// Order-independent pyramid checksum (verification of multi-GPU runs without moving pyramids):
+// sum over every word of every level of splitmix64(global element index * phi + level id * c
+// + float bits), mod 2^64.  Global rows make row-band checksums add up to the whole image's.
+// Restated in numpy by the test suite (tests/test_gpu_parity.py::_checksum).
+__device__ __forceinline__ unsigned long long splitmix_fin(unsigned long long x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+__global__ void __launch_bounds__(kBlock) k_checksum(const Geom* __restrict__ g, const float* __restrict__ out, int b,
+                                                     unsigned long long* __restrict__ sum) {
+    const long long total = g->oct[g->O - 1].grp_begin + (long long)g->oct[g->O - 1].rows * g->oct[g->O - 1].gpr;
+    unsigned long long acc = 0;
+    for (long long t = (long long)blockIdx.x * kBlock + threadIdx.x; t < total; t += (long long)gridDim.x * kBlock) {
+        int o = 0;
+        while (o + 1 < g->O && t >= g->oct[o + 1].grp_begin) ++o;
+        const OctGeom& og = g->oct[o];
+        const long long k = t - og.grp_begin;
+        const int Rl = (int)(k / og.gpr);
+        const int C = 4 * (int)(k - (long long)Rl * og.gpr);
+        const int n = min(4, og.cols - C);
+        const unsigned long long idx0 = (unsigned long long)(og.row0 + Rl) * og.cols + C;
+        const float* p = out + (long long)b * g->pyr_stride + og.lev_off + (long long)Rl * og.cols + C;
+        for (int s = 0; s < g->L; ++s) {
+            const unsigned long long lid = (unsigned long long)(o * 64 + s) * 0xD1B54A32D192ED03ull;
+            for (int j = 0; j < n; ++j) {
+                const unsigned bits = __float_as_uint(p[s * og.lev_stride + j]);
+                acc += splitmix_fin((idx0 + j) * 0x9E3779B97F4A7C15ull + lid + bits);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(sum, acc);
+}
+
 __device__ __forceinline__ unsigned mix32(unsigned x) {
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -431,6 +471,8 @@ struct gdp_ctx {
     const int* d_in = nullptr;    // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
     float* d_taps = nullptr;
+    float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
+    unsigned long long* d_sum = nullptr;
     std::vector<float> h_taps;
     long long in_pitch_own = 0, in_img_stride_own = 0;
     hipStream_t stream = nullptr;
@@ -450,7 +492,11 @@ struct gdp_ctx {
         err = buf;
         return code;
     }
-    hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }
+    // NULL = the context's own stream; GDP_STREAM_NULL ((void*)1) = HIP's default (null) stream
+    hipStream_t pick(void* s) const {
+        if (s == GDP_STREAM_NULL) return (hipStream_t)0;
+        return s ? (hipStream_t)s : stream;
+    }
 };
 
 namespace {
@@ -649,8 +695,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         return hip_fail(e, "hipMalloc(taps)");
     if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(input)");
-    if ((e = hipMalloc(&c->d_out, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
+    if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(pyramid)");
+    c->d_out = c->d_out_own;
+    if ((e = hipMalloc(&c->d_sum, sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(sum)");
     c->d_in = c->d_in_own;
     if ((e = hipMemcpy(c->d_taps, c->h_taps.data(), c->h_taps.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "hipMemcpy(taps)");
@@ -675,7 +723,8 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_geom) (void)hipFree(c->d_geom);
     if (c->d_taps) (void)hipFree(c->d_taps);
     if (c->d_in_own) (void)hipFree(c->d_in_own);
-    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->d_out_own) (void)hipFree(c->d_out_own);
+    if (c->d_sum) (void)hipFree(c->d_sum);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -858,6 +907,42 @@ int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) {
     const long long off = axis == 0 ? og.ctap + (long long)s * og.ctap_stride : og.rtap + (long long)s * og.rtap_stride;
     // read back what the device holds, not the host copy: this is what the kernels use
     GDP_HIP(c, hipMemcpy(host, c->d_taps + off, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return GDP_OK;
+}
+
+int gdp_set_output_device(gdp_ctx* c, float* base, size_t bytes) {
+    if (!c) return GDP_ERR_ARG;
+    if (!base) {
+        c->d_out = c->d_out_own;
+        return GDP_OK;
+    }
+    if (bytes < gdp_pyramid_bytes(c) || (reinterpret_cast<uintptr_t>(base) & 255) != 0)
+        return c->status(GDP_ERR_ARG, "gdp_set_output_device: need >= %zu bytes, 256-B aligned", gdp_pyramid_bytes(c));
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipDeviceSynchronize());
+    c->d_out = base;
+    return GDP_OK;
+}
+
+size_t gdp_level_offset(const gdp_ctx* c, int b, int o, int s) {
+    if (!valid_level(c, b, o, s)) return (size_t)-1;
+    const OctGeom& og = c->geom.oct[o];
+    return (size_t)b * c->geom.pyr_stride + og.lev_off + (size_t)s * og.lev_stride;
+}
+
+int gdp_checksum(gdp_ctx* c, int b, uint64_t* out) {
+    if (!c || !out || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_checksum: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipMemsetAsync(c->d_sum, 0, sizeof(unsigned long long), c->stream));
+    const Geom& g = c->geom;
+    const long long total = g.oct[g.O - 1].grp_begin + (long long)g.oct[g.O - 1].rows * g.oct[g.O - 1].gpr;
+    const int grid = (int)std::max<long long>(1, std::min<long long>((total + kBlock - 1) / kBlock, c->blocks_max));
+    hipLaunchKernelGGL(k_checksum, dim3(grid), dim3(kBlock), 0, c->stream, c->d_geom, c->d_out, b, c->d_sum);
+    GDP_HIP(c, hipGetLastError());
+    unsigned long long v = 0;
+    GDP_HIP(c, hipMemcpyAsync(&v, c->d_sum, sizeof v, hipMemcpyDeviceToHost, c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    *out = v;
     return GDP_OK;
 }
 

@@ -1,0 +1,179 @@
+"""Multi-GPU drivers: one process per GPU over torch.distributed (backend "nccl" = RCCL on ROCm).
+
+The pyramid is pointwise in the input (halo 0) and images are independent, so the work
+partitions with NO data-path collective:
+
+* image sharding (configs 3/4): rank r owns a contiguous block of global image indices;
+* row bands (config 5): rank r owns input rows [r0, r1) of one image, aligned to 2^(max(O,5)-1)
+  rows so every octave's band rows are whole.
+
+Collectives appear only where the caller asks for a result on one rank:
+
+* `generate_dog_mgpu` — the RCCL counterpart of `GaussPyramid_mpi::GenerateDoG_mpi`
+  (GaussDePyramid-MPI.h:265-335).  The reference splits by SCALE (rank i < S+3 filters scale i of
+  every octave and streams rows to collector rank S+3, which does all DoG; needs >= S+4 ranks).
+  Here ranks split by ROW BAND (any world size, DoG fused on every rank) and the collector,
+  rank 0, receives each band's finished pyramid with one gather — the same result on the
+  collector: the full pyramid, bit-identical to the serial reference.
+* `gather_checksums` — 8 bytes per image/band instead of the pyramids (verification at scale).
+
+The band/shard arithmetic and the assembly are pure torch / Python so the N > 1 logic runs under
+`gloo` on CPU in tests (tests/test_distributed.py) with the same code the GPU path uses.
+"""
+import numpy as np
+
+
+def octaves_for(n):
+    x = 0
+    while n > 0:
+        x += 1
+        n //= 2
+    return x
+
+
+# ---------------------------------------------------------------------------------- planning
+def plan_images(total_images, world, rank):
+    """Contiguous block of global image indices for `rank`: (first, count)."""
+    base, extra = divmod(int(total_images), int(world))
+    count = base + (1 if rank < extra else 0)
+    first = rank * base + min(rank, extra)
+    return first, count
+
+
+def band_alignment(octaves):
+    return 1 << (max(int(octaves), 5) - 1)
+
+
+def plan_band(H, world, rank, octaves):
+    """Input rows [r0, r1) of `rank`'s band; every band but the last is a multiple of the
+    alignment, so octave o of band r is rows [r0 >> o, r1 >> o) of the whole image."""
+    align = band_alignment(octaves)
+    per = -(-int(H) // int(world) // align) * align
+    r0 = min(H, rank * per)
+    r1 = min(H, (rank + 1) * per)
+    return r0, r1
+
+
+def band_level_rows(H, octaves, r0, r1):
+    """[(first_row, rows)] per octave for the band [r0, r1) of an H-row image (matches
+    gdp_level_dims of a band context)."""
+    out = []
+    for o in range(octaves):
+        Hg = H >> o
+        first = (r0 + (1 << o) - 1) >> o
+        hi = Hg if r1 == H else min(Hg, (r1 + (1 << o) - 1) >> o)
+        out.append((first, max(0, hi - first)))
+    return out
+
+
+def packed_band_floats(H, W, S, octaves, r0, r1):
+    return sum((S + 3) * rows * (W >> o) for o, (_, rows) in enumerate(band_level_rows(H, octaves, r0, r1)))
+
+
+# ---------------------------------------------------------------------------------- collectives
+def max_over_ranks(values, dist=None, device="cpu"):
+    """Element-wise max of a list of floats over all ranks (the bench's slowest-rank time)."""
+    import torch
+
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def gather_checksums(local, dist=None, dst=0):
+    """Gather each rank's list of 64-bit checksums to rank `dst` (None elsewhere)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [list(local)]
+    out = [None] * dist.get_world_size() if dist.get_rank() == dst else None
+    dist.gather_object(list(local), out, dst=dst)
+    return out
+
+
+def assemble_bands(H, W, S, octaves, world, packed_bands, like=None):
+    """Collector-side assembly: the packed band pyramids of ranks 0..world-1 (torch tensors,
+    any device) -> the packed pyramid of the whole image, in the oracle's [o][s][rows][cols]
+    layout.  Pure device copies; no arithmetic touches the values."""
+    import torch
+
+    total = sum((S + 3) * (H >> o) * (W >> o) for o in range(octaves))
+    ref = like if like is not None else packed_bands[0]
+    full = torch.empty(total, dtype=torch.float32, device=ref.device)
+    layouts = [band_level_rows(H, octaves, *plan_band(H, world, r, octaves)) for r in range(world)]
+    off_full = 0
+    band_off = [0] * world
+    for o in range(octaves):
+        cols = W >> o
+        rows_full = H >> o
+        for s in range(S + 3):
+            for r in range(world):
+                first, rows = layouts[r][o]
+                if rows:
+                    n = rows * cols
+                    dst = off_full + first * cols
+                    full[dst:dst + n] = packed_bands[r][band_off[r]:band_off[r] + n]
+                    band_off[r] += n
+            off_full += rows_full * cols
+    return full
+
+
+def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None):
+    """Collector semantics of GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335) over RCCL.
+
+    Every rank passes the same `img` (the reference also replicates the input on every rank,
+    GaussDePyramid-MPI.h:60-84); rank r builds the row band plan_band(n, world, r, octaves) on its
+    GPU; rank 0 gathers the bands and returns the full packed pyramid (torch tensor, on its GPU);
+    other ranks return None.  `compute(img_band, r0, r1) -> packed float32 torch tensor` may be
+    injected (tests use it to run this logic under gloo on CPU); by default it is the HIP build.
+    """
+    import torch
+
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    O = octaves or octaves_for(n)
+    r0, r1 = plan_band(n, world, rank, O)
+    img = np.asarray(img, dtype=np.int32)[:n, :n]
+    if compute is None:
+        compute = _gpu_band_compute(n, n, S, O, device)
+    band = compute(np.ascontiguousarray(img[r0:r1]), r0, r1)
+    if world == 1:
+        return assemble_bands(n, n, S, O, 1, [band])
+    # equal-size buffers for the gather: pad every band to the largest one
+    sizes = [packed_band_floats(n, n, S, O, *plan_band(n, world, r, O)) for r in range(world)]
+    buf = torch.zeros(max(sizes), dtype=torch.float32, device=band.device)
+    buf[:band.numel()] = band
+    gathered = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gathered, dst=0)
+    if rank != 0:
+        return None
+    return assemble_bands(n, n, S, O, world, [g[:sizes[r]] for r, g in enumerate(gathered)])
+
+
+def _gpu_band_compute(H, W, S, O, device):
+    """Default band compute: a libgdp band context writing straight into a torch tensor."""
+    import torch
+
+    from .gausspyramid import PyramidContext
+
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+
+    def compute(img_band, r0, r1):
+        with PyramidContext(H, W, S=S, octaves=O, batch=1, device=dev.index, row_begin=r0, row_end=r1) as ctx:
+            out = torch.empty(ctx.pyramid_bytes() // 4 + 64, dtype=torch.float32, device=dev)
+            base = out.data_ptr()
+            shift = (-base % 256) // 4  # 256-B aligned view
+            view = out[shift:shift + ctx.pyramid_bytes() // 4]
+            ctx.bind_device_output(view.data_ptr(), ctx.pyramid_bytes(), keepalive=out)
+            ctx.set_input(img_band)
+            ctx.build(torch.cuda.current_stream(dev))
+            parts = []
+            for o in range(O):
+                rows, cols, _ = ctx.level_dims(o)
+                for s in range(S + 3):
+                    off = ctx.level_offset(0, o, s)
+                    parts.append(view[off:off + rows * cols])
+            packed = torch.cat(parts) if parts else view[:0].clone()
+            torch.cuda.current_stream(dev).synchronize()
+            return packed
+
+    return compute

@@ -32,16 +32,19 @@ def _ptr(a):
     return ctypes.c_void_p(a.ctypes.data)
 
 
+GDP_STREAM_NULL = 1  # include/gdp.h: selects HIP's default (null) stream
+
+
 def _stream_handle(stream):
-    """Accept None, an int handle, or a torch.cuda.Stream; return a void* for the C ABI."""
+    """None -> the context's own stream; a torch.cuda.Stream or raw int handle -> that stream
+    (handle 0, torch's default stream, is passed as GDP_STREAM_NULL so it is not mistaken for
+    "the context's stream")."""
     if stream is None:
         return None
-    if isinstance(stream, int):
-        return ctypes.c_void_p(stream)
-    handle = getattr(stream, "cuda_stream", None)
-    if handle is not None:
-        return ctypes.c_void_p(handle)
-    raise TypeError(f"unsupported stream object {stream!r}")
+    handle = stream if isinstance(stream, int) else getattr(stream, "cuda_stream", None)
+    if handle is None:
+        raise TypeError(f"unsupported stream object {stream!r}")
+    return ctypes.c_void_p(handle if handle != 0 else GDP_STREAM_NULL)
 
 
 def octaves_for(n):
@@ -196,6 +199,25 @@ class PyramidContext:
     def levels(self, b=0):
         """{(o, s): 2-D array} of image b."""
         return {(o, s): self.level(b, o, s) for o in range(self.O) for s in range(self.S + 3)}
+
+    def bind_device_output(self, ptr, nbytes, keepalive=None):
+        """Write pyramids into caller device memory (>= pyramid_bytes(), 256-B aligned)."""
+        check(lib().gdp_set_output_device(self._ctx, ctypes.c_void_p(ptr), int(nbytes)), self._ctx)
+        self._out_bound = keepalive
+
+    def unbind_device_output(self):
+        check(lib().gdp_set_output_device(self._ctx, None, 0), self._ctx)
+        self._out_bound = None
+
+    def level_offset(self, b, o, s):
+        """Float offset of level (o, s) of image b inside the (bound or own) pyramid buffer."""
+        return lib().gdp_level_offset(self._ctx, int(b), int(o), int(s))
+
+    def checksum(self, b=0):
+        """Order-independent 64-bit checksum of image b's pyramid (see gdp.h)."""
+        v = ctypes.c_uint64()
+        check(lib().gdp_checksum(self._ctx, int(b), ctypes.byref(v)), self._ctx)
+        return v.value
 
     def device_level_ptr(self, b, o, s):
         return lib().gdp_device_level(self._ctx, int(b), int(o), int(s))

@@ -39,4 +39,6 @@ def golden():
         hashes = json.load(f)
     dumps = dict(np.load(os.path.join(gdir, "dumps.npz"), allow_pickle=False))
     taps = dict(np.load(os.path.join(gdir, "taps.npz"), allow_pickle=False))
-    return {"hashes": hashes, "dumps": dumps, "taps": taps}
+    with open(os.path.join(gdir, "checksums.json")) as f:
+        checksums = json.load(f)
+    return {"hashes": hashes, "dumps": dumps, "taps": taps, "checksums": checksums}

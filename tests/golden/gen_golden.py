@@ -14,6 +14,7 @@ Outputs (all plain data, loadable without pickle):
                 the AVX512xOpenMP subset output, and centre windows for n = 512 / 4096
   taps.npz      the reference's `filter` taps for every (octave, scale) — read from the
                 reference object itself (TapProbe in oracle/ref_harness.cpp)
+  checksums.json gdp_checksum values of the reference's output for the bench inputs
   meta.json     generator provenance (glibc, g++, input definitions)
 
 Usage:  make -C oracle ref && python tests/golden/gen_golden.py
@@ -52,6 +53,9 @@ REGEN_CASES = [(64, 2, "lcg:12345", 2), (64, 2, "lcg:12345", 3), (37, 1, "lcg:5"
 SUBSET_CASES = [(64, 2, "lcg:12345"), (256, 2, "lcg:12345")]
 WINDOW_CASES = [(512, 2, "lcg:12345"), (4096, 2, "lcg:12345")]
 WINDOW = 96
+# bench inputs (config 2/4 image 0 and 1; config 5 image 0) for gdp_checksum fixtures
+CHECKSUM_CASES = [(4096, 2, "synth:0x5EED:0"), (4096, 2, "synth:0x5EED:1"), (512, 2, "lcg:12345"),
+                  (16384, 2, "synth:0x5EED:0")]
 TAP_CASES = [(512, 2), (100, 2), (1000, 2), (513, 3), (4096, 2), (1080, 2), (1920, 2), (37, 1)]
 
 
@@ -143,6 +147,27 @@ def main():
 
     with open(os.path.join(HERE, "hashes.json"), "w") as f:
         json.dump(hashes, f, indent=1)
+
+    # gdp_checksum values (definition in include/gdp.h) of the reference's output for the bench's
+    # own input images, over the first 5 octaves (bench configs) and over all octaves
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # the checksum formula's numpy restatement (test infrastructure)
+
+    checks = []
+    for n, S, inp in CHECKSUM_CASES:
+        pyr = dump(REF_SERIAL, "dump", n, S, inp)
+        sl, _ = level_slices(n, S)
+        acc, rec = 0, {"n": n, "S": S, "input": inp}
+        for o in range(octaves_of(n)):
+            m = n >> o
+            for s in range(S + 3):
+                off, _ = sl[(o, s)]
+                acc = (acc + oracle.level_checksum(pyr[off:off + m * m].reshape(m, m), o, s)) & 0xFFFFFFFFFFFFFFFF
+            rec[f"octaves_{o + 1}"] = f"{acc:016x}"
+        checks.append(rec)
+        print("checksum", n, inp, flush=True)
+    with open(os.path.join(HERE, "checksums.json"), "w") as f:
+        json.dump(checks, f, indent=1)
     gxx = run("g++", "--version").splitlines()[0]
     meta = {
         "generator": "tests/golden/gen_golden.py via oracle/_ref/ref_serial + ref_avx512 "

@@ -316,6 +316,61 @@ def test_config5_16384_bands_equal_whole_image(pkg, oracle):
                 _assert_same(full.level(0, o, s)[r0:r1], want, ("c5 closed form", o, s))
 
 
+# ------------------------------------------------------------------ checksum / zero-copy output / mgpu
+def test_device_checksum_matches_reference(pkg, oracle, golden):
+    """gdp_checksum of the GPU pyramid == the checksum of the reference's own output, incl. the
+    16384^2 config-5 image (whole-image context and the sum of its 8 row bands)."""
+    for rec in golden["checksums"]:
+        n, S, spec = rec["n"], rec["S"], rec["input"]
+        for O in ((5,) if n > 4096 else (1, 5, len([k for k in rec if k.startswith("octaves_")]))):
+            with pkg.PyramidContext(n, n, S=S, octaves=O) as ctx:
+                if spec.startswith("synth:"):
+                    _, seed, idx = spec.split(":")
+                    ctx.fill_synthetic(int(seed, 0), int(idx, 0))
+                else:
+                    ctx.set_input(oracle.image_from_spec(n, spec))
+                ctx.build()
+                assert ctx.checksum(0) == int(rec[f"octaves_{O}"], 16), (n, spec, O)
+        if n == 16384:
+            total = 0
+            for k in range(8):
+                with pkg.PyramidContext(n, n, S=S, octaves=5, row_begin=k * 2048, row_end=(k + 1) * 2048) as band:
+                    band.fill_synthetic(0x5EED, 0)
+                    band.build()
+                    total = (total + band.checksum(0)) & 0xFFFFFFFFFFFFFFFF
+            assert total == int(rec["octaves_5"], 16)
+
+
+def test_output_binding_on_torch_default_stream(pkg, oracle):
+    """Pyramid written straight into a torch tensor, launched on torch's default (null) stream."""
+    import torch
+
+    H, W, S = 80, 144, 2
+    img = oracle.lcg_image(H, W, 31)
+    want = oracle.levels(oracle.build_pyramid(img, S), H, W, S, oracle.default_octaves(H, W))
+    with pkg.PyramidContext(H, W, S=S) as ctx:
+        buf = torch.full((ctx.pyramid_bytes() // 4,), float("nan"), device="cuda")
+        ctx.bind_device_output(buf.data_ptr(), ctx.pyramid_bytes(), keepalive=buf)
+        ctx.set_input(img)
+        ctx.build(torch.cuda.current_stream())  # handle 0 -> GDP_STREAM_NULL
+        torch.cuda.current_stream().synchronize()
+        for (o, s), lev in want.items():
+            off = ctx.level_offset(0, o, s)
+            got = buf[off:off + lev.size].cpu().numpy().reshape(lev.shape)
+            _assert_same(got, lev, ("bound", o, s))
+        ctx.unbind_device_output()
+
+
+def test_generate_dog_mgpu_single_rank(pkg, oracle):
+    import importlib
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    for n, S in [(100, 2), (256, 3)]:
+        img = oracle.lcg_image(n, n, 8)
+        got = d.generate_dog_mgpu(img, n, S)
+        _assert_same(got.cpu().numpy(), oracle.build_pyramid(img, S), ("mgpu", n))
+
+
 # ------------------------------------------------------------------ C++ drop-in driver
 def test_cpp_dropin_driver_matches_reference(oracle, golden, tmp_path):
     exe = os.path.join(REPO, "examples", "main_hip")
