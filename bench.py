@@ -175,6 +175,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override images per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss"],
+                    help="build: fused GaussPyInit+GenerateDoG (headline); regen: in-place GenerateDoG "
+                         "re-entry; gauss: in-place row+column window pass of every octave")
     args = ap.parse_args()
 
     import torch
@@ -224,8 +227,13 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
+    if args.op == "build":
+        step = ctx.build
+    else:
+        ctx.build(stream)  # materialise the pyramid the in-place passes work on
+        step = ctx.generate_dog if args.op == "regen" else (lambda st: ctx.gauss_range(0, O, st))
     for _ in range(args.warmup):
-        ctx.build(stream)
+        step(stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -235,7 +243,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        ctx.build(stream)
+        step(stream)
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -244,16 +252,19 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
     wall, kernel_ms = mg.max_over_ranks([wall, kernel_ms], dist=dist, device=red_dev)
-    parity = verify(ctx, cfg, args.config, world, rank, dist, mg)
+    parity = verify(ctx, cfg, args.config, world, rank, dist, mg) if args.op == "build" else None
 
     # roofline of the (only) kernel of a step, per launch on THIS rank's share
     rows_local = ctx.row_end - ctx.row_begin
-    if cfg["band"]:
-        bytes_launch = 4 * rows_local * W + 4 * (S + 3) * sum(ctx.level_dims(o)[0] * ctx.level_dims(o)[1] for o in range(O))
+    pyr_px = sum(ctx.level_dims(o)[0] * ctx.level_dims(o)[1] for o in range(O)) * (1 if cfg["band"] else B)
+    if args.op != "build":  # in-place passes read and write every level once: 8*(S+3)*P bytes
+        bytes_launch = 8 * (S + 3) * pyr_px
+    elif cfg["band"]:
+        bytes_launch = 4 * rows_local * W + 4 * (S + 3) * pyr_px
     else:
         bytes_launch = algorithmic_bytes(H, W, S, O, B)
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
-    pmc = latest_pmc(args.config)
+    pmc = latest_pmc(args.config) if args.op == "build" else None
 
     result = {
         "metric": METRIC,
@@ -278,12 +289,17 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(pmc["kernel_bytes_per_launch"]) if pmc else None,
-            "kernel": "k_build (fused decimate+window+DoG), variant %d" % ctx.tuning()["variant"],
+            "kernel": ("k_build (fused decimate+window+DoG), variant %d" % ctx.tuning()["variant"]
+                       if args.op == "build" else
+                       {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
+                        "gauss": "k_levels<MODE=1> (in-place row+column window, all octaves)"}[args.op]),
             "kernel_ms": round(kernel_ms, 6),
             "algorithmic_bytes_per_launch": bytes_launch,
         },
     }
-    result["parity"] = parity
+    result["parity"] = parity if args.op == "build" else {"status": "not checked for in-place re-entry ops"}
+    if args.op != "build":
+        result["metric"] = METRIC + f" [op={args.op}: in-place pass]"
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
     elif rank == 0:

@@ -110,6 +110,9 @@ int gdp_init(gdp_ctx* ctx, void* stream);
 /* GaussFilter(o) in place: every scale of octave o *= column window then row window
  * (GuassDePyramid.h:106-134). */
 int gdp_gauss_octave(gdp_ctx* ctx, int octave, void* stream);
+/* GaussFilter(o) for every o in [o_begin, o_end) in ONE launch (the reference calls it per octave
+ * from GenerateDoG, :139); the "row + column window pass" the north star's roofline target names. */
+int gdp_gauss_range(gdp_ctx* ctx, int o_begin, int o_end, void* stream);
 /* DoG of octave o in place: level s -= level s+1 for s = 0..S+1 ascending
  * (GuassDePyramid.h:140-146). */
 int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);

@@ -38,6 +38,7 @@ namespace {
 constexpr int kMaxOct = 32;
 constexpr int kBlock = 256;     // 4 waves (in-place / synthetic kernels)
 constexpr int kTailGroups = 256; // groups of 4 pixels per tail work unit
+constexpr int kLevBlock = 1024;  // threads (= 4-pixel groups) per block of the in-place passes
 constexpr int kFused = 5;       // octaves 0..4 share one 16 x 256 input tile
 constexpr int kTileRows = 16;   // 2^(kFused-1): every fused octave has whole rows in a tile
 constexpr int kTileCols = 256;  // tile width of the register octave-0 path (64 lanes x 4 pixels)
@@ -55,7 +56,23 @@ struct OctGeom {
     int rtap;             // float offset of row taps (o, 0), indexed by GLOBAL output row
     int rtap_stride;
     long long grp_begin;  // prefix (over octaves 0..o-1) of rows*gpr per image
+    unsigned long long gpr_magic; // fast k / gpr for k < 2^31: (k * magic) >> gpr_shift
+    int gpr_shift;
+    int pad_;
 };
+
+// Granlund-Montgomery division by an invariant d >= 1 for numerators n < 2^31:
+// magic = ceil(2^(31+l) / d), l = ceil(log2 d); n / d == (n * magic) >> (31 + l).
+inline void make_magic(unsigned d, unsigned long long* magic, int* shift) {
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    *shift = 31 + l;
+    *magic = ((1ull << *shift) + d - 1) / d;
+}
+
+__device__ __forceinline__ unsigned fast_div(unsigned n, unsigned long long magic, int shift) {
+    return (unsigned)(((unsigned long long)n * magic) >> shift);
+}
 
 struct Geom {
     int H, W, S, L, O, F, batch;
@@ -68,6 +85,7 @@ struct Geom {
     unsigned tiles_per_img, tiles_total;       // host checks the unit count fits 31 bits
     unsigned tail_groups_per_img, tail_units;  // octaves >= F, 256 groups per unit
     OctGeom oct[kMaxOct];
+    unsigned lv_blk[kMaxOct + 1]; // prefix over octaves of ceil(rows*gpr / kLevBlock) per image
 };
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -77,6 +95,15 @@ typedef int i4 __attribute__((ext_vector_type(4)));
 // device helpers
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ f4 ld_f4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+// Streaming load of pyramid data that is read once per pass (in-place passes): non-temporal.
+template <bool NT>
+__device__ __forceinline__ f4 ld_stream(const float* p) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+    else
+        return *reinterpret_cast<const f4*>(p);
+}
 
 template <bool NT>
 __device__ __forceinline__ void st_f4(float* p, f4 v) {
@@ -298,66 +325,120 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // In-place passes over octaves [o_begin, o_end) of every image (GaussPyInit refill, GaussFilter,
 // DoG, GenerateDoG re-entry).  MODE bits: 1 = window multiply (GaussFilter), 2 = DoG subtract,
-// 4 = refill from the input (GaussPyInit; exclusive).
-template <int LT, int MODE>
-__global__ void __launch_bounds__(kBlock) k_inplace(const Geom* __restrict__ g, const int* __restrict__ in,
-                                                    float* __restrict__ out, const float* __restrict__ taps,
-                                                    int o_begin, int o_end) {
+// 4 = refill from the input (GaussPyInit; exclusive).  One block = kLevBlock consecutive groups
+// (4 pixels each) of one octave's level rows; every thread owns one group across all S+3 levels:
+// the S+3 float4 loads are issued together (LT known), then the rolling window/DoG and the stores.
+template <int LT, int MODE, bool NT>
+__global__ void __launch_bounds__(kLevBlock) k_levels(const Geom* __restrict__ g, const int* __restrict__ in,
+                                                      float* __restrict__ out, const float* __restrict__ taps,
+                                                      int o_begin, int o_end) {
+    const unsigned first = g->lv_blk[o_begin];
+    const unsigned per = g->lv_blk[o_end] - first;
+    const unsigned b = blockIdx.x / per;
+    const unsigned v = blockIdx.x - b * per + first;
+    int o = o_begin;
+    while (o + 1 < o_end && v >= g->lv_blk[o + 1]) ++o;
+    const OctGeom og = g->oct[o];
+    const unsigned k = (v - g->lv_blk[o]) * kLevBlock + threadIdx.x;
+    if (k >= (unsigned)og.rows * (unsigned)og.gpr) return;
+    const int Rl = (int)fast_div(k, og.gpr_magic, og.gpr_shift);
+    const int C = 4 * (int)(k - (unsigned)Rl * (unsigned)og.gpr);
+    const int n = min(4, og.cols - C);
+    const bool full = (n == 4) && ((og.cols & 3) == 0);
+    float* p = out + (long long)b * g->pyr_stride + og.lev_off + (long long)Rl * og.cols + C;
     const int L = LT > 0 ? LT : g->L;
-    const long long first = g->oct[o_begin].grp_begin;
-    const long long per = (o_end < g->O ? g->oct[o_end].grp_begin
-                                        : g->oct[g->O - 1].grp_begin +
-                                              (long long)g->oct[g->O - 1].rows * g->oct[g->O - 1].gpr) -
-                          first;
-    const long long total = per * g->batch;
-    for (long long t = (long long)blockIdx.x * kBlock + threadIdx.x; t < total; t += (long long)gridDim.x * kBlock) {
-        const int b = (int)(t / per);
-        const long long rem = t - (long long)b * per + first;
-        int o = o_begin;
-        while (o + 1 < o_end && rem >= g->oct[o + 1].grp_begin) ++o;
-        const OctGeom og = g->oct[o];
-        const long long k = rem - og.grp_begin;
-        const int Rl = (int)(k / og.gpr);
-        const int C = 4 * (int)(k - (long long)Rl * og.gpr);
-        const int n = min(4, og.cols - C);
-        const bool full = (n == 4) && ((og.cols & 3) == 0);
-        float* p = out + (long long)b * g->pyr_stride + og.lev_off + (long long)Rl * og.cols + C;
-        auto ld = [&](int s) -> f4 {
-            const float* q = p + s * og.lev_stride;
-            if (full) return ld_f4(q);
-            f4 v = {q[0], 0.f, 0.f, 0.f};
-            if (n > 1) v.y = q[1];
-            if (n > 2) v.z = q[2];
-            if (n > 3) v.w = q[3];
-            return v;
+    auto ld = [&](int s) -> f4 {
+        const float* q = p + s * og.lev_stride;
+        if (full) return ld_stream<NT>(q);
+        f4 r = {q[0], 0.f, 0.f, 0.f};
+        if (n > 1) r.y = q[1];
+        if (n > 2) r.z = q[2];
+        if (n > 3) r.w = q[3];
+        return r;
+    };
+    auto st = [&](int s, f4 val) {
+        if (full)
+            st_f4<NT>(p + s * og.lev_stride, val);
+        else
+            st_part(p + s * og.lev_stride, val, n, false);
+    };
+    if constexpr (MODE == 4) {
+        const f4 x = load_px(g, in, (int)b, o, og.row0 + Rl, C, n);
+        for (int s = 0; s < L; ++s) st(s, x);
+    } else {
+        const int Rg = og.row0 + Rl;
+        const float* ct = taps + og.ctap + C;
+        const float* rt = taps + og.rtap + Rg;
+        auto win = [&](int s, f4 val) -> f4 {
+            if constexpr ((MODE & 1) != 0) return (val * ld_f4(ct + s * og.ctap_stride)) * rt[s * og.rtap_stride];
+            return val;
         };
-        auto st = [&](int s, f4 v) { st_part(p + s * og.lev_stride, v, n, full); };
-        if constexpr (MODE == 4) {
-            const f4 x = load_px(g, in, b, o, og.row0 + Rl, C, n);
+        if constexpr (LT > 0) {
+            f4 x[LT];
 #pragma unroll
-            for (int s = 0; s < L; ++s) st(s, x);
-        } else {
-            const int Rg = og.row0 + Rl;
-            const float* ct = taps + og.ctap + C;
-            const float* rt = taps + og.rtap + Rg;
-            auto win = [&](int s, f4 v) -> f4 {
-                if constexpr ((MODE & 1) != 0) return (v * ld_f4(ct + s * og.ctap_stride)) * rt[s * og.rtap_stride];
-                return v;
-            };
+            for (int s = 0; s < LT; ++s) x[s] = ld(s);
             if constexpr (MODE == 1) {
 #pragma unroll
-                for (int s = 0; s < L; ++s) st(s, win(s, ld(s)));
+                for (int s = 0; s < LT; ++s) st(s, win(s, x[s]));
             } else {
-                f4 gp = win(0, ld(0));
+                f4 gp = win(0, x[0]);
 #pragma unroll
-                for (int s = 0; s + 1 < L; ++s) {
-                    const f4 gn = win(s + 1, ld(s + 1));
+                for (int s = 0; s + 1 < LT; ++s) {
+                    const f4 gn = win(s + 1, x[s + 1]);
                     st(s, gp - gn);
                     gp = gn;
                 }
-                if constexpr ((MODE & 1) != 0) st(L - 1, gp);
+                if constexpr ((MODE & 1) != 0) st(LT - 1, gp);
             }
+        } else if constexpr (MODE == 1) {
+            for (int s = 0; s < L; ++s) st(s, win(s, ld(s)));
+        } else {
+            f4 gp = win(0, ld(0));
+            for (int s = 0; s + 1 < L; ++s) {
+                const f4 gn = win(s + 1, ld(s + 1));
+                st(s, gp - gn);
+                gp = gn;
+            }
+            if constexpr ((MODE & 1) != 0) st(L - 1, gp);
         }
+    }
+}
+
+// GaussFilter pass (MODE 1 of the in-place passes) with one LEVEL per block slice: the levels of
+// an octave are independent under the window, so every thread moves exactly one float4 (load,
+// two multiplies, store) — the shape that streams best in place on MI355X (tools/membench:
+// 1 float4 per lane with non-temporal load+store ≈ 6.5 TB/s vs ≈ 6.1 at 4 per lane).
+template <bool NT>
+__global__ void __launch_bounds__(kLevBlock) k_window(const Geom* __restrict__ g, float* __restrict__ out,
+                                                      const float* __restrict__ taps, int o_begin, int o_end) {
+    const unsigned L = (unsigned)g->L;
+    const unsigned first = g->lv_blk[o_begin] * L;
+    const unsigned per = g->lv_blk[o_end] * L - first;
+    const unsigned b = blockIdx.x / per;
+    const unsigned v = blockIdx.x - b * per + first;
+    int o = o_begin;
+    while (o + 1 < o_end && v >= g->lv_blk[o + 1] * L) ++o;
+    const OctGeom og = g->oct[o];
+    const unsigned nb = g->lv_blk[o + 1] - g->lv_blk[o]; // blocks per level of octave o
+    const unsigned w = v - g->lv_blk[o] * L;
+    const int s = (int)(w / nb);
+    const unsigned k = (w - (unsigned)s * nb) * kLevBlock + threadIdx.x;
+    if (k >= (unsigned)og.rows * (unsigned)og.gpr) return;
+    const int Rl = (int)fast_div(k, og.gpr_magic, og.gpr_shift);
+    const int C = 4 * (int)(k - (unsigned)Rl * (unsigned)og.gpr);
+    const int n = min(4, og.cols - C);
+    const bool full = (n == 4) && ((og.cols & 3) == 0);
+    float* p = out + (long long)b * g->pyr_stride + og.lev_off + (long long)s * og.lev_stride + (long long)Rl * og.cols + C;
+    const f4 fc = ld_f4(taps + og.ctap + s * og.ctap_stride + C);
+    const float fr = taps[og.rtap + s * og.rtap_stride + og.row0 + Rl];
+    if (full) {
+        st_f4<NT>(p, (ld_stream<NT>(p) * fc) * fr);
+    } else {
+        f4 r = {p[0], 0.f, 0.f, 0.f};
+        if (n > 1) r.y = p[1];
+        if (n > 2) r.z = p[2];
+        if (n > 3) r.w = p[3];
+        st_part(p, (r * fc) * fr, n, false);
     }
 }
 
@@ -546,17 +627,24 @@ int launch_build(gdp_ctx* c, hipStream_t st) {
 template <int MODE>
 int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     const Geom& g = c->geom;
-    const long long end = oe < g.O ? g.oct[oe].grp_begin
-                                   : g.oct[g.O - 1].grp_begin + (long long)g.oct[g.O - 1].rows * g.oct[g.O - 1].gpr;
-    const long long total = (end - g.oct[ob].grp_begin) * g.batch;
-    if (total <= 0) return GDP_OK;
-    const int grid = (int)std::min<long long>((total + kBlock - 1) / kBlock, c->blocks_max);
-    if (g.L == 5)
-        hipLaunchKernelGGL((k_inplace<5, MODE>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
-                           c->d_taps, ob, oe);
-    else
-        hipLaunchKernelGGL((k_inplace<0, MODE>), dim3(grid), dim3(kBlock), 0, st, c->d_geom, c->d_in, c->d_out,
-                           c->d_taps, ob, oe);
+    if constexpr (MODE == 1) {
+        const long long grid = ((long long)g.lv_blk[oe] - g.lv_blk[ob]) * g.L * g.batch;
+        if (grid <= 0) return GDP_OK;
+        if (grid >= (1ll << 31) || (long long)g.lv_blk[g.O] * g.L >= (1ll << 32))
+            return c->status(GDP_ERR_ARG, "window pass too large for one launch");
+        hipLaunchKernelGGL(c->nontemporal ? k_window<true> : k_window<false>, dim3((unsigned)grid), dim3(kLevBlock), 0, st,
+                           c->d_geom, c->d_out, c->d_taps, ob, oe);
+        GDP_HIP(c, hipGetLastError());
+        return GDP_OK;
+    }
+    const long long per = (long long)g.lv_blk[oe] - g.lv_blk[ob];
+    const long long grid = per * g.batch;
+    if (grid <= 0) return GDP_OK;
+    if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "in-place pass too large for one launch");
+    auto kern = g.L == 5 ? (c->nontemporal ? k_levels<5, MODE, true> : k_levels<5, MODE, false>)
+                         : (c->nontemporal ? k_levels<0, MODE, true> : k_levels<0, MODE, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kLevBlock), 0, st, c->d_geom, c->d_in, c->d_out, c->d_taps, ob,
+                       oe);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
 }
@@ -659,7 +747,9 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         og.rtap = (int)tap_off;
         tap_off += (long long)og.rtap_stride * g.L;
         og.grp_begin = grp;
+        make_magic((unsigned)std::max(1, og.gpr), &og.gpr_magic, &og.gpr_shift);
         grp += (long long)og.rows * og.gpr;
+        g.lv_blk[o + 1] = g.lv_blk[o] + (unsigned)(((long long)og.rows * og.gpr + kLevBlock - 1) / kLevBlock);
     }
     g.pyr_stride = round_up(lev_off, kLevelAlign);
     const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
@@ -828,6 +918,12 @@ int gdp_gauss_octave(gdp_ctx* c, int o, void* stream) {
     if (!c || o < 0 || o >= c->geom.O) return c ? c->status(GDP_ERR_ARG, "octave out of range") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<1>(c, o, o + 1, c->pick(stream));
+}
+
+int gdp_gauss_range(gdp_ctx* c, int ob, int oe, void* stream) {
+    if (!c || ob < 0 || oe > c->geom.O || ob >= oe) return c ? c->status(GDP_ERR_ARG, "octave range invalid") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<1>(c, ob, oe, c->pick(stream));
 }
 
 int gdp_dog_octave(gdp_ctx* c, int o, void* stream) {

@@ -131,6 +131,11 @@ class PyramidContext:
     def gauss_octave(self, o, stream=None):
         check(lib().gdp_gauss_octave(self._ctx, int(o), _stream_handle(stream)), self._ctx)
 
+    def gauss_range(self, o_begin=0, o_end=None, stream=None):
+        """GaussFilter of octaves [o_begin, o_end) in one launch (in place)."""
+        o_end = self.O if o_end is None else o_end
+        check(lib().gdp_gauss_range(self._ctx, int(o_begin), int(o_end), _stream_handle(stream)), self._ctx)
+
     def dog_octave(self, o, stream=None):
         check(lib().gdp_dog_octave(self._ctx, int(o), _stream_handle(stream)), self._ctx)
 

@@ -231,6 +231,28 @@ def test_inplace_ops_match_reference_order(pkg, oracle):
         _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
 
 
+@pytest.mark.parametrize("nt", [1, 0])
+def test_gauss_range_and_store_modes(pkg, oracle, nt):
+    """One-launch GaussFilter over an octave range == per-octave GaussFilter; both store modes;
+    a batch of 3 and a generic-S (S = 4) context."""
+    for H, W, S, B in [(90, 200, 2, 3), (64, 48, 4, 1)]:
+        O = oracle.default_octaves(H, W)
+        imgs = [oracle.lcg_image(H, W, 5 + b) for b in range(B)]
+        with pkg.PyramidContext(H, W, S=S, batch=B) as ctx:
+            ctx.set_tuning(nontemporal=nt)
+            for b, img in enumerate(imgs):
+                ctx.set_input(img, b)
+            ctx.init()
+            ctx.gauss_range(1, O)
+            ctx.generate_dog()
+            for b, img in enumerate(imgs):
+                want = oracle.init_pyramid(img, S)
+                for o in range(1, O):
+                    oracle.gauss_octave(want, H, W, S, o)
+                oracle.generate_dog(want, H, W, S, O)
+                _assert_same(ctx.pyramid(b), want, ("gauss_range", H, W, S, b, nt))
+
+
 def test_generate_dog_reentry_vs_reference(pkg, oracle, golden):
     for name, arr in golden["dumps"].items():
         if not name.startswith("regen_"):

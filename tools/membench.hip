@@ -62,6 +62,38 @@ __global__ void k_write_chunk(f4* __restrict__ p) {
     }
 }
 
+// in-place scale, one block = 256 lanes x PER float4, reads issued before writes; LNT = nt loads
+template <bool NT, bool LNT, int PER>
+__global__ void k_scale_chunk(f4* __restrict__ p) {
+    f4* q = p + (long)blockIdx.x * 256 * PER + threadIdx.x;
+    f4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = LNT ? __builtin_nontemporal_load(q + k * 256) : q[k * 256];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if constexpr (NT)
+            __builtin_nontemporal_store(v[k] * 1.0001f, q + k * 256);
+        else
+            q[k * 256] = v[k] * 1.0001f;
+    }
+}
+
+// out-of-place copy, one block = 256 lanes x PER float4
+template <bool NT, int PER>
+__global__ void k_copy_chunk(const f4* __restrict__ a, f4* __restrict__ b) {
+    const long base = (long)blockIdx.x * 256 * PER + threadIdx.x;
+    f4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = a[base + k * 256];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if constexpr (NT)
+            __builtin_nontemporal_store(v[k], b + base + k * 256);
+        else
+            b[base + k * 256] = v[k];
+    }
+}
+
 // n int4 reads, 5 x n float4 writes into 5 separate arrays (the k_build octave-0 shape)
 template <bool NT>
 __global__ void k_r1w5(const i4* __restrict__ in, f4* __restrict__ out, long n) {
@@ -119,6 +151,15 @@ int main() {
         rep("chunk4_plain", bytes, time_it([&] { k_write_chunk<false, 4><<<n / 1024, 256>>>(a); }, reps));
         rep("chunk16_nt", bytes, time_it([&] { k_write_chunk<true, 16><<<n / 4096, 256>>>(a); }, reps));
         rep("chunk1_nt", bytes, time_it([&] { k_write_chunk<true, 1><<<n / 256, 256>>>(a); }, reps));
+        rep("scale1_nt", 2.0 * bytes, time_it([&] { k_scale_chunk<true, false, 1><<<n / 256, 256>>>(a); }, reps));
+        rep("scale1_plain", 2.0 * bytes, time_it([&] { k_scale_chunk<false, false, 1><<<n / 256, 256>>>(a); }, reps));
+        rep("scale1_ntld_nt", 2.0 * bytes, time_it([&] { k_scale_chunk<true, true, 1><<<n / 256, 256>>>(a); }, reps));
+        rep("scale4_nt", 2.0 * bytes, time_it([&] { k_scale_chunk<true, false, 4><<<n / 1024, 256>>>(a); }, reps));
+        rep("scale4_ntld_nt", 2.0 * bytes, time_it([&] { k_scale_chunk<true, true, 4><<<n / 1024, 256>>>(a); }, reps));
+        rep("scale4_plain", 2.0 * bytes, time_it([&] { k_scale_chunk<false, false, 4><<<n / 1024, 256>>>(a); }, reps));
+        rep("copy1_nt", 2.0 * bytes, time_it([&] { k_copy_chunk<true, 1><<<n / 256, 256>>>(b, a); }, reps));
+        rep("copy4_nt", 2.0 * bytes, time_it([&] { k_copy_chunk<true, 4><<<n / 1024, 256>>>(b, a); }, reps));
+        rep("copy4_plain", 2.0 * bytes, time_it([&] { k_copy_chunk<false, 4><<<n / 1024, 256>>>(b, a); }, reps));
         rep("chunk4_nt_2GB", 4.0 * bytes, time_it([&] { k_write_chunk<true, 4><<<4 * n / 1024, 256>>>(a); }, reps));
         rep("chunk4_plain_2GB", 4.0 * bytes, time_it([&] { k_write_chunk<false, 4><<<4 * n / 1024, 256>>>(a); }, reps));
     }

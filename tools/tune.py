@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss"])
     ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
     args = ap.parse_args()
     pkg = entry.load_package()
@@ -59,11 +60,27 @@ def main():
         if ref is None:
             ref = lev
         assert np.array_equal(lev.view(np.uint32), ref.view(np.uint32)), name
+    import torch
+
+    stream = torch.cuda.Stream()
+    step = {"build": ctx.build, "regen": ctx.generate_dog, "gauss": lambda st: ctx.gauss_range(0, O, st)}[args.op]
     for _ in range(args.rounds):
         for name, kw in variants:
             apply(kw)
-            times[name].append(ctx.time_builds(args.iters) / args.iters)
-    nbytes = bench.algorithmic_bytes(H, W, 2, O, B)
+            if args.op == "build":
+                times[name].append(ctx.time_builds(args.iters) / args.iters)
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.iters):
+                    step(stream)
+                e1.record(stream)
+                e1.synchronize()
+                times[name].append(e0.elapsed_time(e1) / args.iters)
+    if args.op == "build":
+        nbytes = bench.algorithmic_bytes(H, W, 2, O, B)
+    else:
+        nbytes = 8 * 5 * B * sum((H >> o) * (W >> o) for o in range(O))
     for name, _ in variants:
         t = np.array(times[name])
         print(json.dumps({"variant": name, "config": args.config, "ms_median": round(float(np.median(t)), 5),
