@@ -1,0 +1,105 @@
+// GaussDePyramid-HIP-mpitest.h — drop-in for the free-function / global-state API of the
+// reference's mpitest.cpp (GaussPyInit(int* data[MAX]) :438-473, GenerateDoG_mpi :114-189,
+// GenerateDoG_mpi_omp :35-113, delete_mpi :474-493, globals :26-34), running on one MI355X through
+// libgdp (gdp.h).  Like mpitest.cpp itself, it DEFINES the globals and functions, so include it in
+// exactly one translation unit, in place of those definitions; link -lgdp.
+//
+// Semantics kept: GaussPy[layer][S+3][len_o][len_o] host arrays, n/length/layer/S globals,
+// GaussPyInit refills from data[k<<o][l<<o], GenerateDoG_* leave the finished pyramid (DoG levels
+// 0..S+1, Gaussian S+2) in GaussPy and print the elapsed seconds like the collector rank does
+// (mpitest.cpp:95-96, :171-172).  The reference's MPI fan-out over S+3 worker ranks is replaced by
+// the GPU; the functions can be called repeatedly (no MPI_Init/MPI_Finalize inside).
+// Note: mpitest.cpp's window centre is float(len-1)/2 (:44); this build uses the serial
+// GuassDePyramid.h centre (float length halved, :107-115) — identical for power-of-two n, which is
+// the only size mpitest.cpp runs (n = 256, :548).
+#ifndef SIFT_GAUSSDEPYRAMID_HIP_MPITEST_H
+#define SIFT_GAUSSDEPYRAMID_HIP_MPITEST_H
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+
+#include "gdp.h"
+
+#ifndef GDP_MPITEST_MAX
+#define GDP_MPITEST_MAX 4096  // mpitest.cpp:28
+#endif
+
+int thread_count = 4;  // mpitest.cpp:26 (unused on the GPU)
+int chunk_size = 5;    // :27 (unused)
+const int MAX = GDP_MPITEST_MAX;
+int n = 128;  // :29
+int S = 2;    // :30
+float**** GaussPy;
+int length = n;
+int layer = 0;
+bool is_initialized = false;
+static gdp_ctx* gdp_mpitest_ctx = nullptr;
+static bool gdp_mpitest_fresh = false;
+
+static inline void gdp_mpitest_check(int status, const char* what) {
+    if (status != GDP_OK) {
+        std::fprintf(stderr, "%s failed: %s (%s)\n", what, gdp_status_string(status), gdp_last_error(gdp_mpitest_ctx));
+        std::abort();
+    }
+}
+
+// :438-473 — first call allocates GaussPy (and the device context); every call refills.
+void GaussPyInit(int* data[MAX]) {
+    length = n;
+    if (!is_initialized) {
+        layer = gdp_octaves_for(length);
+        GaussPy = new float***[layer];
+        for (int o = 0; o < layer; ++o) {
+            GaussPy[o] = new float**[S + 3];
+            for (int s = 0; s < S + 3; ++s) {
+                GaussPy[o][s] = new float*[length >> o];
+                for (int r = 0; r < (length >> o); ++r) GaussPy[o][s][r] = new float[length >> o];
+            }
+        }
+        gdp_mpitest_check(gdp_create(&gdp_mpitest_ctx, length, length, S, layer, 1, 0), "GaussPyInit");
+    }
+    is_initialized = true;
+    gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
+    gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
+    for (int o = 0; o < layer; ++o)
+        for (int s = 0; s < S + 3; ++s)
+            gdp_mpitest_check(gdp_download_level_rows(gdp_mpitest_ctx, 0, o, s, GaussPy[o][s]), "GaussPyInit");
+    gdp_mpitest_fresh = true;
+}
+
+static inline void gdp_mpitest_generate() {
+    auto begin = std::chrono::steady_clock::now();
+    gdp_mpitest_check(gdp_mpitest_fresh ? gdp_build(gdp_mpitest_ctx, nullptr) : gdp_generate_dog(gdp_mpitest_ctx, nullptr),
+                      "GenerateDoG_mpi");
+    gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");
+    gdp_mpitest_fresh = false;
+    for (int o = 0; o < layer; ++o)
+        for (int s = 0; s < S + 3; ++s)
+            gdp_mpitest_check(gdp_download_level_rows(gdp_mpitest_ctx, 0, o, s, GaussPy[o][s]), "GenerateDoG_mpi");
+    auto end = std::chrono::steady_clock::now();
+    std::cout << std::chrono::duration<double>(end - begin).count() << std::endl;
+}
+
+void GenerateDoG_mpi(int, char**) { gdp_mpitest_generate(); }      // :114-189
+void GenerateDoG_mpi_omp(int, char**) { gdp_mpitest_generate(); }  // :35-113
+
+// :474-493
+void delete_mpi() {
+    if (!is_initialized) return;
+    for (int o = 0; o < layer; ++o) {
+        for (int s = 0; s < S + 3; ++s) {
+            for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
+            delete[] GaussPy[o][s];
+        }
+        delete[] GaussPy[o];
+    }
+    delete[] GaussPy;
+    gdp_destroy(gdp_mpitest_ctx);
+    gdp_mpitest_ctx = nullptr;
+    is_initialized = false;
+    layer = 0;
+}
+
+#endif  // SIFT_GAUSSDEPYRAMID_HIP_MPITEST_H

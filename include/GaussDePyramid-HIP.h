@@ -41,6 +41,11 @@ public:
     void output();
     void GaussFilter(int theLayer);
     void GenerateDoG();
+    // GaussPyramid_mpi::GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335), the call main.cpp:68 makes.
+    // The reference fans scales out over >= S+4 MPI ranks and collects on rank S+3; here one GPU
+    // does the whole pyramid, so the result every caller sees is the collector's.  Unlike the
+    // reference (MPI_Init/MPI_Finalize inside) it may be called any number of times.
+    void GenerateDoG_mpi(int argc, char** argv);
     ~GaussPyramid_hip();
     bool initialized;
     bool mirror_host;  // copy the pyramid into GaussPy after every mutating call (default true)
@@ -118,6 +123,8 @@ inline void GaussPyramid_hip::GenerateDoG() {
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG");
     if (mirror_host) SyncHost();
 }
+
+inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) { GenerateDoG(); }
 
 inline void GaussPyramid_hip::output() {  // :89-104
     int len = length;

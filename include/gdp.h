@@ -121,7 +121,9 @@ int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);
  * like the reference's repeated-call timing loop (main.cpp:66-73). */
 int gdp_generate_dog(gdp_ctx* ctx, void* stream);
 
-/* ---- output -------------------------------------------------------------------------------- */
+/* ---- output --------------------------------------------------------------------------------
+ * The blocking copies below are ordered after work on the context's OWN stream; if a build was
+ * launched on another stream, synchronize that stream first. */
 /* Device pointer to level (o, s) of image b: rows x cols float32, row-major, dense. */
 const float* gdp_device_level(const gdp_ctx* ctx, int b, int octave, int scale);
 /* Copy level (o, s) of image b to a dense host array (blocking). */

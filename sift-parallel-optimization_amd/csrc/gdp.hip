@@ -553,6 +553,8 @@ struct gdp_ctx {
     float* d_out = nullptr;
     float* d_taps = nullptr;
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
+    float* h_stage = nullptr;     // pinned staging for row-pointer downloads (largest level)
+    size_t h_stage_floats = 0;
     unsigned long long* d_sum = nullptr;
     std::vector<float> h_taps;
     long long in_pitch_own = 0, in_img_stride_own = 0;
@@ -814,6 +816,7 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_taps) (void)hipFree(c->d_taps);
     if (c->d_in_own) (void)hipFree(c->d_in_own);
     if (c->d_out_own) (void)hipFree(c->d_out_own);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->d_sum) (void)hipFree(c->d_sum);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -957,10 +960,19 @@ int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) {
 int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows) {
     if (!valid_level(c, b, o, s) || !rows) return c ? c->status(GDP_ERR_ARG, "gdp_download_level_rows: bad argument") : GDP_ERR_ARG;
     const OctGeom& og = c->geom.oct[o];
-    std::vector<float> tmp((size_t)og.rows * og.cols);
-    int rc = gdp_download_level(c, b, o, s, tmp.data());
-    if (rc != GDP_OK) return rc;
-    for (int r = 0; r < og.rows; ++r) std::memcpy(rows[r], tmp.data() + (size_t)r * og.cols, (size_t)og.cols * 4);
+    const size_t nfl = (size_t)og.rows * og.cols;
+    if (nfl == 0) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    if (c->h_stage_floats < nfl) {  // one pinned buffer, grown to the largest level requested
+        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->h_stage_floats = 0;
+        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, nfl * 4, hipHostMallocDefault));
+        c->h_stage_floats = nfl;
+    }
+    GDP_HIP(c, hipMemcpyAsync(c->h_stage, gdp_device_level(c, b, o, s), nfl * 4, hipMemcpyDeviceToHost, c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    for (int r = 0; r < og.rows; ++r) std::memcpy(rows[r], c->h_stage + (size_t)r * og.cols, (size_t)og.cols * 4);
     return GDP_OK;
 }
 

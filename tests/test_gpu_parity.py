@@ -408,5 +408,18 @@ def test_cpp_dropin_driver_matches_reference(oracle, golden, tmp_path):
             assert oracle.fnv(lv[(o, s)]) == int(h, 16), (o, s)
     subprocess.run([exe, "64", "2", "lcg:12345", str(out), "3"], check=True, timeout=120)
     _assert_same(np.fromfile(out, dtype=np.float32), golden["dumps"]["regen_64_2_lcg-12345_3"], "driver regen x3")
-    timing = subprocess.run([exe], check=True, timeout=120, capture_output=True, text=True).stdout
-    assert float(timing.strip()) > 0
+    timing = subprocess.run([exe], check=True, timeout=120, capture_output=True, text=True).stdout.splitlines()
+    assert len(timing) == 2 and all(float(t.split()[0]) > 0 for t in timing), timing
+
+
+def test_cpp_mpitest_dropin_matches_oracle(oracle, tmp_path):
+    """mpitest.cpp's free-function API (GaussPyInit(int**), GenerateDoG_mpi_omp, delete_mpi)."""
+    exe = os.path.join(REPO, "examples", "mpitest_hip")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
+    out = tmp_path / "m.f32"
+    for n, spec in [(256, "lcg:12345"), (256, "ones"), (100, "lcg:3")]:
+        r = subprocess.run([exe, str(n), spec, str(out)], check=True, timeout=120, capture_output=True, text=True)
+        assert float(r.stdout.split()[0]) >= 0  # elapsed seconds, printed like the collector rank
+        _assert_same(np.fromfile(out, dtype=np.float32), oracle.build_pyramid(oracle.image_from_spec(n, spec), 2),
+                     ("mpitest", n, spec))
