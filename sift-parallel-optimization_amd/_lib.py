@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("GDP_LIBRARY", os.path.join(PKG_DIR, "lib", "libgdp.so
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "gdp.h")
 
 GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV = range(6)
-GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT = 1, 2, 3, 4
+GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT, GDP_TUNE_TILE_ORDER = 1, 2, 3, 4, 5
 
 
 class GdpError(RuntimeError):

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -78,7 +79,7 @@ struct Geom {
     int H, W, S, L, O, F, batch;
     int in_rows, in_row0; // input rows held (band) and their first global row
     int vec_in;           // 16-B int4 input loads legal (pitch % 4 == 0, base aligned)
-    int pad_;
+    int tile_order;       // GDP_TUNE_TILE_ORDER
     long long in_pitch, in_img_stride;
     long long pyr_stride; // floats between image pyramids
     int tiles_r, tiles_c;
@@ -237,8 +238,20 @@ __device__ __forceinline__ void build_body(const Geom* __restrict__ g, const int
     const int F = g->F;
     for (unsigned u = blockIdx.x; u < units; u += gridDim.x) {
         if (u < tiles_total) {
-            const unsigned b = u / g->tiles_per_img;
-            const unsigned rem = u - b * g->tiles_per_img;
+            // tile order: 0 = linear; 1 = XCD-chunked (blocks b and b+8 share an XCD under the
+            // observed round-robin dispatch, so XCD x walks the contiguous tile range x/8 of the
+            // grid) — a speed knob only, any order gives the same bits
+            unsigned t = u;
+            if (g->tile_order == 1 && (tiles_total & 7u) == 0) {
+                t = (u & 7u) * (tiles_total >> 3) + (u >> 3);
+            } else if (g->tile_order == 2 && ((tiles_total / (unsigned)g->tiles_c) & 7u) == 0) {
+                // XCD row-interleave: XCD x sweeps whole tile rows x, x+8, ... left to right
+                const unsigned k = u >> 3, tcs = (unsigned)g->tiles_c;
+                const unsigned q = k / tcs;
+                t = (q * 8u + (u & 7u)) * tcs + (k - q * tcs);
+            }
+            const unsigned b = t / g->tiles_per_img;
+            const unsigned rem = t - b * g->tiles_per_img;
             const unsigned tr = rem / (unsigned)g->tiles_c;
             const unsigned tc = rem - tr * (unsigned)g->tiles_c;
             const int in_r0 = (int)tr * kTileRows; // band-local input row of the tile
@@ -729,6 +742,9 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     c->in_pitch_own = g.in_pitch;
     c->in_img_stride_own = g.in_img_stride;
 
+    // optional padding between levels (floats, multiple of 64) — layout experiment knob
+    const char* pad_env = std::getenv("GDP_LEVEL_PAD");
+    const long long level_pad = pad_env ? round_up(std::max(0ll, std::atoll(pad_env)), kLevelAlign) : 0;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
     long long tap_off = 0, lev_off = 0, grp = 0;
     for (int o = 0; o < O; ++o) {
@@ -739,7 +755,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         og.rows = std::max(0, row_hi - og.row0);
         og.cols = W >> o;
         og.gpr = (og.cols + 3) / 4;
-        og.lev_stride = round_up((long long)og.rows * og.cols, kLevelAlign);
+        og.lev_stride = round_up((long long)og.rows * og.cols, kLevelAlign) + level_pad;
         og.lev_off = lev_off;
         lev_off += og.lev_stride * g.L;
         og.ctap_stride = (int)round_up(og.cols, 4);
@@ -764,6 +780,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     }
     g.tail_groups_per_img = (unsigned)tail_per_img;
     g.tail_units = (unsigned)tail_units;
+    // Tile order default (tools/tune.py, MI355X): a single very large image (>= 64 Mpix, e.g. the
+    // 16384^2 config) streams 7-8 % faster when each XCD sweeps its own contiguous eighth of the
+    // tiles; batches and <= 4096^2 images are fastest in linear order.
+    g.tile_order = (batch == 1 && (long long)g.in_rows * W >= (1ll << 26)) ? 1 : 0;
     retile(c, kVariants[c->variant].tile_cols);
     c->h_taps.assign((size_t)tap_off, 0.0f);
     for (int o = 0; o < O; ++o) {
@@ -1070,6 +1090,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_BLOCKS_PER_CU: *value = c->persistent ? c->blocks_max / c->cus : 0; return GDP_OK;
         case GDP_TUNE_GRID: *value = c->grid_override; return GDP_OK;
         case GDP_TUNE_VARIANT: *value = c->variant; return GDP_OK;
+        case GDP_TUNE_TILE_ORDER: *value = c->geom.tile_order; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 }
@@ -1089,6 +1110,10 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             if (value < 0) return c->status(GDP_ERR_ARG, "grid must be >= 0");
             c->grid_override = value;
             return GDP_OK;
+        case GDP_TUNE_TILE_ORDER:
+            if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");
+            c->geom.tile_order = value;
+            return upload_geom(c);
         case GDP_TUNE_VARIANT: {
             if (value < 0 || value >= kNumVariants) return c->status(GDP_ERR_ARG, "variant out of range");
             const int old = c->variant;

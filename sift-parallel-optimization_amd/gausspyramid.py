@@ -149,22 +149,24 @@ class PyramidContext:
     def stream(self):
         return lib().gdp_stream(self._ctx)
 
-    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None):
+    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None):
         """Performance knobs of the build kernel (outputs are bit-identical for every setting)."""
-        from ._lib import GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_VARIANT
+        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_TILE_ORDER,
+                           GDP_TUNE_VARIANT)
 
         for key, val in ((GDP_TUNE_NONTEMPORAL, nontemporal), (GDP_TUNE_BLOCKS_PER_CU, blocks_per_cu),
-                         (GDP_TUNE_GRID, grid), (GDP_TUNE_VARIANT, variant)):
+                         (GDP_TUNE_GRID, grid), (GDP_TUNE_VARIANT, variant), (GDP_TUNE_TILE_ORDER, tile_order)):
             if val is not None:
                 check(lib().gdp_set_tuning(self._ctx, key, int(val)), self._ctx)
 
     def tuning(self):
         """Current {nontemporal, blocks_per_cu, grid, variant} of the build kernel."""
-        from ._lib import GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_VARIANT
+        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_TILE_ORDER,
+                           GDP_TUNE_VARIANT)
 
         out = {}
         for name, key in (("nontemporal", GDP_TUNE_NONTEMPORAL), ("blocks_per_cu", GDP_TUNE_BLOCKS_PER_CU),
-                          ("grid", GDP_TUNE_GRID), ("variant", GDP_TUNE_VARIANT)):
+                          ("grid", GDP_TUNE_GRID), ("variant", GDP_TUNE_VARIANT), ("tile_order", GDP_TUNE_TILE_ORDER)):
             v = _i()
             check(lib().gdp_get_tuning(self._ctx, key, ctypes.byref(v)), self._ctx)
             out[name] = v.value

@@ -116,12 +116,13 @@ def test_build_matches_oracle_shapes(pkg, oracle, H, W, S, O):
 def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
     """Every code variant of the build kernel (block size / tile width / octave-0 path, also
     persistent grids and plain stores) produces identical bits."""
-    for H, W, S, O in [(100, 300, 2, 0), (67, 1000, 3, 5), (256, 512, 2, 9), (33, 65, 1, 0)]:
+    for H, W, S, O in [(100, 300, 2, 0), (67, 1000, 3, 5), (256, 512, 2, 9), (33, 65, 1, 0), (128, 1024, 2, 5)]:
         img = oracle.lcg_image(H, W, 77 + variant)
         want = oracle.build_pyramid(img, S, O or None)
         with pkg.PyramidContext(H, W, S=S, octaves=O) as ctx:
             ctx.set_input(img)
-            for kw in ({"variant": variant}, {"nontemporal": 0}, {"blocks_per_cu": 1}, {"grid": 3}):
+            for kw in ({"variant": variant}, {"tile_order": 1}, {"tile_order": 2}, {"nontemporal": 0},
+                       {"blocks_per_cu": 1}, {"grid": 3}):
                 ctx.set_tuning(**kw)
                 ctx.build()
                 _assert_same(ctx.pyramid(0), want, (variant, H, W, S, O, kw))

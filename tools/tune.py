@@ -40,7 +40,10 @@ def main():
     for v in args.variants.split(";"):
         kv = dict(p.split("=") for p in v.split(","))
         variants.append((v, {"nontemporal": int(kv.get("nt", 1)), "grid": int(kv.get("grid", "0"), 0),
-                             "variant": int(kv.get("v", 0))}))
+                             "variant": int(kv.get("v", -1)) if "v" in kv else None,
+                             "tile_order": int(kv.get("ord", 0))}))
+        if variants[-1][1]["variant"] is None:
+            del variants[-1][1]["variant"]
         if "bpc" in kv:
             variants[-1][1]["blocks_per_cu"] = int(kv["bpc"])
     times = {name: [] for name, _ in variants}
