@@ -44,9 +44,10 @@ def pyramid_pixels(H, W, O, rows=None):
     return sum(((rows if rows is not None else H) >> o) * (W >> o) for o in range(O))
 
 
-def algorithmic_bytes(H, W, S, O, batch):
-    """B = 4*H*W (read every input pixel once) + 4*(S+3)*P (write the final pyramid once)."""
-    return batch * (4 * H * W + 4 * (S + 3) * pyramid_pixels(H, W, O))
+def algorithmic_bytes(H, W, S, O, batch, in_bytes=4):
+    """B = 4*H*W (read every int32 input pixel once; 1*H*W for uint8 input) + 4*(S+3)*P (write the
+    final pyramid once)."""
+    return batch * (in_bytes * H * W + 4 * (S + 3) * pyramid_pixels(H, W, O))
 
 
 def cpu_info():
@@ -175,6 +176,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override images per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--input", default="i32", choices=["i32", "u8"],
+                    help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss"],
                     help="build: fused GaussPyInit+GenerateDoG (headline); regen: in-place GenerateDoG "
                          "re-entry; gauss: in-place row+column window pass of every octave")
@@ -213,12 +216,13 @@ def main():
     if cfg["band"]:
         # one image, row bands aligned to 2^(max(O,5)-1) rows: each rank owns rows [r0, r1)
         r0, r1 = mg.plan_band(H, world, rank, O)
-        ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=1, device=local, row_begin=r0, row_end=r1)
+        ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=1, device=local, row_begin=r0, row_end=r1,
+                                 input_format=args.input)
         ctx.fill_synthetic(SEED, 0)
         scaling = "strong"
         units_all = H * W  # input pixels of the whole job per step
     else:
-        ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, device=local)
+        ctx = pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, device=local, input_format=args.input)
         ctx.fill_synthetic(SEED, rank * B)  # rank r owns global images [r*B, (r+1)*B)
         scaling = "weak"
         units_all = world * B * H * W
@@ -256,15 +260,16 @@ def main():
 
     # roofline of the (only) kernel of a step, per launch on THIS rank's share
     rows_local = ctx.row_end - ctx.row_begin
+    in_bytes = 1 if args.input == "u8" else 4
     pyr_px = sum(ctx.level_dims(o)[0] * ctx.level_dims(o)[1] for o in range(O)) * (1 if cfg["band"] else B)
     if args.op != "build":  # in-place passes read and write every level once: 8*(S+3)*P bytes
         bytes_launch = 8 * (S + 3) * pyr_px
     elif cfg["band"]:
-        bytes_launch = 4 * rows_local * W + 4 * (S + 3) * pyr_px
+        bytes_launch = in_bytes * rows_local * W + 4 * (S + 3) * pyr_px
     else:
-        bytes_launch = algorithmic_bytes(H, W, S, O, B)
+        bytes_launch = algorithmic_bytes(H, W, S, O, B, in_bytes)
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
-    pmc = latest_pmc(args.config) if args.op == "build" else None
+    pmc = latest_pmc(args.config) if args.op == "build" and args.input == "i32" else None
 
     result = {
         "metric": METRIC,
@@ -284,6 +289,7 @@ def main():
             "images_per_gpu": 1 if cfg["band"] else B,
             "parallelism": (f"row-band x{world}" if cfg["band"] else f"image-sharded x{world}"),
             "input_mpix_per_step": units_all / 1e6,
+            "input_format": "int32" if args.input == "i32" else "uint8",
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -94,6 +94,14 @@ int gdp_set_input_host(gdp_ctx* ctx, int b, const int32_t* base, size_t pitch, v
  * at base + b*image_stride + r*pitch (int32 elements).  Pass base = NULL to go back to the
  * context's own input buffer.  The memory must stay valid while builds run. */
 int gdp_set_input_device(gdp_ctx* ctx, const int32_t* base, size_t pitch, size_t image_stride);
+/* Input pixel format of the context: GDP_INPUT_I32 (default; the reference's int) or
+ * GDP_INPUT_U8 (8-bit images: a quarter of the input bytes, identical pyramid bits since every
+ * uint8 value is an int).  Switching reallocates the context's input buffer (contents zeroed). */
+enum { GDP_INPUT_I32 = 0, GDP_INPUT_U8 = 1 };
+int gdp_set_input_format(gdp_ctx* ctx, int format);
+int gdp_get_input_format(const gdp_ctx* ctx);
+int gdp_set_input_host_u8(gdp_ctx* ctx, int b, const uint8_t* base, size_t pitch, void* stream);
+int gdp_set_input_device_u8(gdp_ctx* ctx, const uint8_t* base, size_t pitch, size_t image_stride);
 /* Benchmark/test input generated on the device (SURVEY.md §8d counter hash): image b of the
  * batch gets global index first_image + b; pixel = lowbias32(seed ^ fold(idx)) >> 24 with
  * idx = (index*H + r)*W + c over the WHOLE image (band contexts generate their rows only). */

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("GDP_LIBRARY", os.path.join(PKG_DIR, "lib", "libgdp.so
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "gdp.h")
 
 GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV = range(6)
+GDP_INPUT_I32, GDP_INPUT_U8 = 0, 1
 GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT, GDP_TUNE_TILE_ORDER = 1, 2, 3, 4, 5
 
 
@@ -48,6 +49,10 @@ SIGNATURES = {
     "gdp_set_input_rows": (_c_int, [_p, _c_int, _p, _p]),
     "gdp_set_input_host": (_c_int, [_p, _c_int, _p, _c_size, _p]),
     "gdp_set_input_device": (_c_int, [_p, _p, _c_size, _c_size]),
+    "gdp_set_input_format": (_c_int, [_p, _c_int]),
+    "gdp_get_input_format": (_c_int, [_p]),
+    "gdp_set_input_host_u8": (_c_int, [_p, _c_int, _p, _c_size, _p]),
+    "gdp_set_input_device_u8": (_c_int, [_p, _p, _c_size, _c_size]),
     "gdp_fill_synthetic": (_c_int, [_p, _c_u32, _c_long, _p]),
     "gdp_build": (_c_int, [_p, _p]),
     "gdp_init": (_c_int, [_p, _p]),

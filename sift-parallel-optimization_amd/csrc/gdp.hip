@@ -78,8 +78,10 @@ __device__ __forceinline__ unsigned fast_div(unsigned n, unsigned long long magi
 struct Geom {
     int H, W, S, L, O, F, batch;
     int in_rows, in_row0; // input rows held (band) and their first global row
-    int vec_in;           // 16-B int4 input loads legal (pitch % 4 == 0, base aligned)
+    int vec_in;           // one vector load per 4 pixels legal (pitch % 4 == 0, base aligned)
     int tile_order;       // GDP_TUNE_TILE_ORDER
+    int in_fmt;           // GDP_INPUT_I32 / GDP_INPUT_U8
+    int pad2_;
     long long in_pitch, in_img_stride;
     long long pyr_stride; // floats between image pyramids
     int tiles_r, tiles_c;
@@ -126,16 +128,36 @@ __device__ __forceinline__ void st_part(float* p, f4 v, int n, bool aligned_full
     if (n > 3) p[3] = v.w;
 }
 
-// Input pixels (R, C..C+3) of octave o for image b as float (zero beyond the row end).
-__device__ __forceinline__ f4 load_px(const Geom* __restrict__ g, const int* __restrict__ in, int b, int o,
+// Input pixels (R, C..C+3) of octave o for image b as float (zero beyond the row end).  The
+// input is int32 (the reference's `int** img`) or uint8 (GDP_INPUT_U8: 4x fewer input bytes);
+// the format is a wave-uniform scalar branch.  (float) of an int32 or uint8 value is the same
+// single rounding the reference's `GaussPy[..] = data[..]` assignment performs (:80).
+__device__ __forceinline__ f4 load_px(const Geom* __restrict__ g, const void* __restrict__ in, int b, int o,
                                       int Rg, int C, int n) {
     const long long in_row = ((long long)Rg << o) - g->in_row0;
-    const int* row = in + (long long)b * g->in_img_stride + in_row * g->in_pitch;
+    const long long row_off = (long long)b * g->in_img_stride + in_row * g->in_pitch;
+    f4 x = {0.f, 0.f, 0.f, 0.f};
+    if (g->in_fmt == GDP_INPUT_U8) {
+        const unsigned char* row = static_cast<const unsigned char*>(in) + row_off;
+        if (o == 0 && n == 4 && g->vec_in) {
+            const unsigned w = *reinterpret_cast<const unsigned*>(row + C);
+            x.x = (float)(w & 0xffu);
+            x.y = (float)((w >> 8) & 0xffu);
+            x.z = (float)((w >> 16) & 0xffu);
+            x.w = (float)(w >> 24);
+            return x;
+        }
+        x.x = (float)row[(long long)C << o];
+        if (n > 1) x.y = (float)row[(long long)(C + 1) << o];
+        if (n > 2) x.z = (float)row[(long long)(C + 2) << o];
+        if (n > 3) x.w = (float)row[(long long)(C + 3) << o];
+        return x;
+    }
+    const int* row = static_cast<const int*>(in) + row_off;
     if (o == 0 && n == 4 && g->vec_in) {
         const i4 v = *reinterpret_cast<const i4*>(row + C);
         return __builtin_convertvector(v, f4);
     }
-    f4 x = {0.f, 0.f, 0.f, 0.f};
     x.x = (float)row[(long long)C << o];
     if (n > 1) x.y = (float)row[(long long)(C + 1) << o];
     if (n > 2) x.z = (float)row[(long long)(C + 2) << o];
@@ -146,7 +168,7 @@ __device__ __forceinline__ f4 load_px(const Geom* __restrict__ g, const int* __r
 // One group = 4 consecutive output pixels (Rl, C..C+3) of octave o, all S+3 scales.
 // G_s = (x * fc_s) * fr_s ; out_s = G_s - G_{s+1} ; out_{L-1} = G_{L-1}.
 template <int LT, bool NT>
-__device__ __forceinline__ void build_group(const Geom* __restrict__ g, const int* __restrict__ in,
+__device__ __forceinline__ void build_group(const Geom* __restrict__ g, const void* __restrict__ in,
                                             float* __restrict__ out, const float* __restrict__ taps, int b,
                                             int o, const OctGeom& og, int Rl, int C) {
     const int L = LT > 0 ? LT : g->L;
@@ -180,7 +202,7 @@ __device__ __forceinline__ void build_group(const Geom* __restrict__ g, const in
 // (scalar loads); the 4 int4 input loads are issued before any arithmetic.  Every wave store is
 // 64 lanes x 16 B = 1 KiB contiguous of one level row.
 template <int LT, bool NT>
-__device__ __forceinline__ void tile_octave0(const Geom* __restrict__ g, const int* __restrict__ in,
+__device__ __forceinline__ void tile_octave0(const Geom* __restrict__ g, const void* __restrict__ in,
                                              float* __restrict__ out, const float* __restrict__ taps, int b,
                                              int in_r0, int in_c0) {
     const OctGeom og = g->oct[0];
@@ -231,7 +253,7 @@ __device__ __forceinline__ void tile_octave0(const Geom* __restrict__ g, const i
 // retire, which measured faster than a persistent grid); the grid-stride loop serves capped grids.
 // BLK = threads per block; O0REG selects the register-resident octave-0 path (BLK = 256 only).
 template <int LT, bool NT, int BLK, int TC, bool O0REG>
-__device__ __forceinline__ void build_body(const Geom* __restrict__ g, const int* __restrict__ in,
+__device__ __forceinline__ void build_body(const Geom* __restrict__ g, const void* __restrict__ in,
                                            float* __restrict__ out, const float* __restrict__ taps) {
     const unsigned tiles_total = g->tiles_total;
     const unsigned units = tiles_total + g->tail_units;
@@ -301,7 +323,7 @@ __device__ __forceinline__ void build_body(const Geom* __restrict__ g, const int
 }
 
 template <int LT, bool NT, int BLK, int TC, bool O0REG>
-__global__ void __launch_bounds__(BLK) k_build(const Geom* __restrict__ g, const int* __restrict__ in,
+__global__ void __launch_bounds__(BLK) k_build(const Geom* __restrict__ g, const void* __restrict__ in,
                                                float* __restrict__ out, const float* __restrict__ taps) {
     build_body<LT, NT, BLK, TC, O0REG>(g, in, out, taps);
 }
@@ -309,7 +331,7 @@ __global__ void __launch_bounds__(BLK) k_build(const Geom* __restrict__ g, const
 // Build-kernel code variants (GDP_TUNE_VARIANT); all bit-identical, A/B'd by tools/tune.py.
 struct BuildVariant {
     int block, tile_cols;
-    void (*k[2][2])(const Geom*, const int*, float*, const float*); // [LT==5][NT]
+    void (*k[2][2])(const Geom*, const void*, float*, const float*); // [LT==5][NT]
 };
 #define GDP_VARIANT(BLK, TC, REG)                                                                \
     BuildVariant {                                                                               \
@@ -342,7 +364,7 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 // (4 pixels each) of one octave's level rows; every thread owns one group across all S+3 levels:
 // the S+3 float4 loads are issued together (LT known), then the rolling window/DoG and the stores.
 template <int LT, int MODE, bool NT>
-__global__ void __launch_bounds__(kLevBlock) k_levels(const Geom* __restrict__ g, const int* __restrict__ in,
+__global__ void __launch_bounds__(kLevBlock) k_levels(const Geom* __restrict__ g, const void* __restrict__ in,
                                                       float* __restrict__ out, const float* __restrict__ taps,
                                                       int o_begin, int o_end) {
     const unsigned first = g->lv_blk[o_begin];
@@ -505,7 +527,7 @@ __device__ __forceinline__ unsigned mix32(unsigned x) {
 }
 
 // Counter-hash synthetic images, generated in place on each GPU.
-__global__ void __launch_bounds__(kBlock) k_synth(const Geom* __restrict__ g, int* __restrict__ in, unsigned seed,
+__global__ void __launch_bounds__(kBlock) k_synth(const Geom* __restrict__ g, void* __restrict__ in, unsigned seed,
                                                   long long first_image) {
     const long long W = g->W;
     const long long per = (long long)g->in_rows * W;
@@ -519,7 +541,12 @@ __global__ void __launch_bounds__(kBlock) k_synth(const Geom* __restrict__ g, in
             ((unsigned long long)(first_image + b) * (unsigned long long)g->H + (unsigned long long)(g->in_row0 + r)) *
                 (unsigned long long)W +
             (unsigned long long)c;
-        in[b * g->in_img_stride + r * g->in_pitch + c] = (int)(mix32(seed ^ (unsigned)(idx ^ (idx >> 32))) >> 24);
+        const unsigned px = mix32(seed ^ (unsigned)(idx ^ (idx >> 32))) >> 24;
+        const long long off = b * g->in_img_stride + r * g->in_pitch + c;
+        if (g->in_fmt == GDP_INPUT_U8)
+            static_cast<unsigned char*>(in)[off] = (unsigned char)px;
+        else
+            static_cast<int*>(in)[off] = (int)px;
     }
 }
 
@@ -561,8 +588,8 @@ struct gdp_ctx {
     int device = 0;
     Geom geom{};
     Geom* d_geom = nullptr;
-    int* d_in_own = nullptr;      // context-owned input buffer
-    const int* d_in = nullptr;    // buffer the kernels read (own or caller's)
+    void* d_in_own = nullptr;     // context-owned input buffer (int32 or uint8 per geom.in_fmt)
+    const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
     float* d_taps = nullptr;
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
@@ -805,7 +832,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     if ((e = hipMalloc(&c->d_geom, sizeof(Geom))) != hipSuccess) return hip_fail(e, "hipMalloc(geom)");
     if ((e = hipMalloc(&c->d_taps, std::max<size_t>(4, c->h_taps.size() * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(taps)");
-    if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)
+    if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)  // int32
         return hip_fail(e, "hipMalloc(input)");
     if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(pyramid)");
@@ -869,22 +896,58 @@ size_t gdp_packed_floats(const gdp_ctx* c) {
     return n;
 }
 
-int gdp_set_input_host(gdp_ctx* c, int b, const int32_t* base, size_t pitch, void* stream) {
+namespace {
+size_t in_elem_size(const gdp_ctx* c) { return c->geom.in_fmt == GDP_INPUT_U8 ? 1 : 4; }
+
+int upload_input(gdp_ctx* c, int b, const void* base, size_t pitch, int fmt, void* stream, const char* who) {
     if (!c || !base || b < 0 || b >= c->geom.batch || pitch < (size_t)c->geom.W)
-        return c ? c->status(GDP_ERR_ARG, "gdp_set_input_host: bad argument") : GDP_ERR_ARG;
-    if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
+        return c ? c->status(GDP_ERR_ARG, "%s: bad argument", who) : GDP_ERR_ARG;
+    if (c->geom.in_fmt != fmt) return c->status(GDP_ERR_STATE, "%s: context input format differs (gdp_set_input_format)", who);
+    if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "%s: input is bound to caller device memory", who);
+    const size_t esz = in_elem_size(c);
     GDP_HIP(c, hipSetDevice(c->device));
     hipStream_t st = c->pick(stream);
-    GDP_HIP(c, hipMemcpy2DAsync(c->d_in_own + (size_t)b * c->geom.in_img_stride, (size_t)c->geom.in_pitch * 4, base,
-                                pitch * 4, (size_t)c->geom.W * 4, (size_t)c->geom.in_rows, hipMemcpyHostToDevice, st));
+    GDP_HIP(c, hipMemcpy2DAsync(static_cast<char*>(c->d_in_own) + (size_t)b * c->geom.in_img_stride * esz,
+                                (size_t)c->geom.in_pitch * esz, base, pitch * esz, (size_t)c->geom.W * esz,
+                                (size_t)c->geom.in_rows, hipMemcpyHostToDevice, st));
     GDP_HIP(c, hipStreamSynchronize(st));
     return GDP_OK;
+}
+
+int bind_input(gdp_ctx* c, const void* base, size_t pitch, size_t image_stride, int fmt, const char* who) {
+    if (!c) return GDP_ERR_ARG;
+    Geom& g = c->geom;
+    if (!base) {
+        c->d_in = c->d_in_own;
+        g.in_pitch = c->in_pitch_own;
+        g.in_img_stride = c->in_img_stride_own;
+        g.vec_in = 1;
+        return upload_geom(c);
+    }
+    if (g.in_fmt != fmt) return c->status(GDP_ERR_STATE, "%s: context input format differs (gdp_set_input_format)", who);
+    if (pitch < (size_t)g.W || (g.batch > 1 && image_stride < pitch * (size_t)g.in_rows))
+        return c->status(GDP_ERR_ARG, "%s: pitch/image_stride too small", who);
+    const uintptr_t align = fmt == GDP_INPUT_U8 ? 3 : 15; // one uchar4 / int4 load per 4 pixels
+    c->d_in = base;
+    g.in_pitch = (long long)pitch;
+    g.in_img_stride = (long long)image_stride;
+    g.vec_in = ((reinterpret_cast<uintptr_t>(base) & align) == 0 && pitch % 4 == 0 && image_stride % 4 == 0) ? 1 : 0;
+    return upload_geom(c);
+}
+}  // namespace
+
+int gdp_set_input_host(gdp_ctx* c, int b, const int32_t* base, size_t pitch, void* stream) {
+    return upload_input(c, b, base, pitch, GDP_INPUT_I32, stream, "gdp_set_input_host");
+}
+
+int gdp_set_input_host_u8(gdp_ctx* c, int b, const uint8_t* base, size_t pitch, void* stream) {
+    return upload_input(c, b, base, pitch, GDP_INPUT_U8, stream, "gdp_set_input_host_u8");
 }
 
 int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stream) {
     if (!c || !rows || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_set_input_rows: bad argument") : GDP_ERR_ARG;
     if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
-    // Gather the row pointers into one pinned staging image, then one 2-D copy.
+    // Gather the row pointers into one staging image, then one 2-D copy.
     const size_t W = (size_t)c->geom.W, R = (size_t)c->geom.in_rows;
     std::vector<int32_t> stage(W * R);
     for (size_t r = 0; r < R; ++r) {
@@ -895,23 +958,30 @@ int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stre
 }
 
 int gdp_set_input_device(gdp_ctx* c, const int32_t* base, size_t pitch, size_t image_stride) {
-    if (!c) return GDP_ERR_ARG;
-    Geom& g = c->geom;
-    if (!base) {
-        c->d_in = c->d_in_own;
-        g.in_pitch = c->in_pitch_own;
-        g.in_img_stride = c->in_img_stride_own;
-        g.vec_in = 1;
-        return upload_geom(c);
-    }
-    if (pitch < (size_t)g.W || (g.batch > 1 && image_stride < pitch * (size_t)g.in_rows))
-        return c->status(GDP_ERR_ARG, "gdp_set_input_device: pitch/image_stride too small");
-    c->d_in = base;
-    g.in_pitch = (long long)pitch;
-    g.in_img_stride = (long long)image_stride;
-    g.vec_in = ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && pitch % 4 == 0 && image_stride % 4 == 0) ? 1 : 0;
-    return upload_geom(c);
+    return bind_input(c, base, pitch, image_stride, GDP_INPUT_I32, "gdp_set_input_device");
 }
+
+int gdp_set_input_device_u8(gdp_ctx* c, const uint8_t* base, size_t pitch, size_t image_stride) {
+    return bind_input(c, base, pitch, image_stride, GDP_INPUT_U8, "gdp_set_input_device_u8");
+}
+
+int gdp_set_input_format(gdp_ctx* c, int fmt) {
+    if (!c || (fmt != GDP_INPUT_I32 && fmt != GDP_INPUT_U8)) return c ? c->status(GDP_ERR_ARG, "unknown input format") : GDP_ERR_ARG;
+    if (fmt == c->geom.in_fmt) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipDeviceSynchronize());
+    const size_t bytes = (size_t)c->in_img_stride_own * c->geom.batch * (fmt == GDP_INPUT_U8 ? 1 : 4);
+    void* fresh = nullptr;
+    hipError_t e = hipMalloc(&fresh, std::max<size_t>(16, bytes));
+    if (e != hipSuccess) return c->status(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, "hipMalloc(input)");
+    GDP_HIP(c, hipMemset(fresh, 0, std::max<size_t>(16, bytes)));
+    GDP_HIP(c, hipFree(c->d_in_own));
+    c->d_in_own = fresh;
+    c->geom.in_fmt = fmt;
+    return bind_input(c, nullptr, 0, 0, fmt, "gdp_set_input_format");
+}
+
+int gdp_get_input_format(const gdp_ctx* c) { return c ? c->geom.in_fmt : -1; }
 
 int gdp_fill_synthetic(gdp_ctx* c, uint32_t seed, long first_image, void* stream) {
     if (!c) return GDP_ERR_ARG;

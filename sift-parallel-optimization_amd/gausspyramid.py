@@ -59,7 +59,8 @@ class PyramidContext:
     All compute calls are asynchronous on `stream` (None = the context's own stream).
     """
 
-    def __init__(self, height, width, S=2, octaves=0, batch=1, device=0, row_begin=0, row_end=None):
+    def __init__(self, height, width, S=2, octaves=0, batch=1, device=0, row_begin=0, row_end=None,
+                 input_format="i32"):
         L = lib()
         self._ctx = ctypes.c_void_p()
         row_end = height if row_end is None else row_end
@@ -76,6 +77,17 @@ class PyramidContext:
             check(L.gdp_level_dims(self._ctx, o, ctypes.byref(r), ctypes.byref(c), ctypes.byref(f)), self._ctx)
             self._dims.append((r.value, c.value, f.value))
         self._bound = None  # keeps a caller's device input alive
+        self.input_format = "i32"
+        if input_format != "i32":
+            self.set_input_format(input_format)
+
+    def set_input_format(self, fmt):
+        """'i32' (the reference's int pixels) or 'u8' (8-bit images, 4x fewer input bytes)."""
+        from ._lib import GDP_INPUT_I32, GDP_INPUT_U8
+
+        code = {"i32": GDP_INPUT_I32, "u8": GDP_INPUT_U8}[fmt]
+        check(lib().gdp_set_input_format(self._ctx, code), self._ctx)
+        self.input_format = fmt
 
     # ------------------------------------------------------------------ geometry
     @property
@@ -94,12 +106,18 @@ class PyramidContext:
 
     # ------------------------------------------------------------------ input
     def set_input(self, img, b=0, stream=None):
-        """Upload one H x W (band: band-rows x W) int32 image from host memory."""
-        img = np.ascontiguousarray(img, dtype=np.int32)
+        """Upload one H x W (band: band-rows x W) image from host memory, in the context's input
+        format (int32, or uint8 for an input_format='u8' context)."""
+        u8 = self.input_format == "u8"
+        img = np.asarray(img)
+        if u8 and img.dtype != np.uint8:
+            raise TypeError("a u8 context takes uint8 images")
+        img = np.ascontiguousarray(img, dtype=np.uint8 if u8 else np.int32)
         rows = self.row_end - self.row_begin
         if img.ndim != 2 or img.shape[1] != self.W or img.shape[0] != rows:
             raise ValueError(f"expected a ({rows}, {self.W}) image, got {img.shape}")
-        check(lib().gdp_set_input_host(self._ctx, int(b), _ptr(img), self.W, _stream_handle(stream)), self._ctx)
+        fn = lib().gdp_set_input_host_u8 if u8 else lib().gdp_set_input_host
+        check(fn(self._ctx, int(b), _ptr(img), self.W, _stream_handle(stream)), self._ctx)
 
     def set_input_rows(self, rows, b=0, stream=None):
         """Upload from a list of row arrays — the reference ctor's `int** img` (GuassDePyramid.h:38-46)."""
@@ -108,8 +126,10 @@ class PyramidContext:
         check(lib().gdp_set_input_rows(self._ctx, int(b), ptrs, _stream_handle(stream)), self._ctx)
 
     def bind_device_input(self, ptr, pitch, image_stride, keepalive=None):
-        """Read images straight from caller device memory (int32 elements for pitch/stride)."""
-        check(lib().gdp_set_input_device(self._ctx, ctypes.c_void_p(ptr), int(pitch), int(image_stride)), self._ctx)
+        """Read images straight from caller device memory (pitch/stride in elements of the
+        context's input format)."""
+        fn = lib().gdp_set_input_device_u8 if self.input_format == "u8" else lib().gdp_set_input_device
+        check(fn(self._ctx, ctypes.c_void_p(ptr), int(pitch), int(image_stride)), self._ctx)
         self._bound = keepalive
 
     def unbind_device_input(self):

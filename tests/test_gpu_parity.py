@@ -202,6 +202,38 @@ def test_device_input_binding(pkg, oracle):
             ctx.unbind_device_input()
 
 
+def test_uint8_input_format(pkg, oracle):
+    """8-bit input (host upload, device binding aligned / unaligned, device generator): the same
+    pyramid bits as the int32 image with the same values."""
+    import torch
+
+    for H, W in [(96, 128), (50, 37), (1080, 1920)]:
+        img = oracle.lcg_image(H, W, 4).astype(np.uint8)
+        want = oracle.build_pyramid(img.astype(np.int32), 2, 5 if H > 500 else None)
+        with pkg.PyramidContext(H, W, S=2, octaves=5 if H > 500 else 0, input_format="u8") as ctx:
+            ctx.set_input(img)
+            ctx.build()
+            _assert_same(ctx.pyramid(0), want, ("u8 host", H, W))
+            for pitch in (W, W + 3, ((W + 63) // 64) * 64):
+                host = np.zeros((H, pitch), np.uint8)
+                host[:, :W] = img
+                dev = torch.from_numpy(host).cuda()
+                ctx.bind_device_input(dev.data_ptr(), pitch, H * pitch, keepalive=dev)
+                ctx.build(torch.cuda.current_stream())
+                torch.cuda.synchronize()
+                _assert_same(ctx.pyramid(0), want, ("u8 device", H, W, pitch))
+                ctx.unbind_device_input()
+    with pkg.PyramidContext(256, 512, S=2, batch=2, input_format="u8") as a, \
+            pkg.PyramidContext(256, 512, S=2, batch=2) as b:
+        for c in (a, b):
+            c.fill_synthetic(0x5EED, 3)
+            c.build()
+        for i in range(2):
+            assert a.checksum(i) == b.checksum(i)
+        with pytest.raises(TypeError):
+            a.set_input(np.zeros((256, 512), np.int32))
+
+
 def test_int_star_star_upload(pkg, oracle):
     img = oracle.lcg_image(40, 40, 1)
     with pkg.PyramidContext(40, 40, S=2) as ctx:
