@@ -1,0 +1,220 @@
+// GaussDePyramid-HIP-mpi.h — drop-in for `class GaussPyramid_mpi` (GaussDePyramid-MPI.h:16-53):
+// the multi-process variant, with MPI kept only as the launcher/bootstrap and the pyramid built on
+// one MI355X per rank and collected over RCCL (xGMI) by libgdp_comm (gdp_comm.h).
+//
+//     #include "GaussDePyramid-HIP-mpi.h"         // was "GaussDePyramid-MPI.h"
+//     GaussPyramid_hip_mpi g(p, n, 2);           // was GaussPyramid_mpi
+//     g.GenerateDoG_mpi(argc, argv);             // main.cpp:68, under mpiexec -n <ranks>
+//
+// Build: g++ -I<repo>/include -I/opt/conda/include main.cpp -L<lib> -lgdp_comm -lgdp
+//        -L/opt/conda/lib -lmpi   (any MPI; it only launches ranks and broadcasts 128 bytes)
+//
+// Semantics.  The reference's GenerateDoG_mpi needs >= S+4 ranks: ranks i < S+3 filter scale i
+// of every octave and send each row to rank S+3, the collector, which forms all DoG levels
+// (:265-335); the collector's GaussPy ends as the full pyramid.  Here ANY number of ranks works:
+// rank r builds row band gdp_band_rows(n, size, r, layer) of every level on GPU r % devices,
+// and rank 0 — the collector — receives every band into its whole-image context and mirrors it
+// into GaussPy; other ranks' GaussPy keep their GaussPyInit contents (the reference's workers
+// also end with partial data).  Bit-identical to GuassDePyramid.h's GenerateDoG on the collector.
+// Differences: MPI is initialised once (if the caller has not) and finalised by the destructor,
+// so GenerateDoG_mpi may be called repeatedly (the reference calls MPI_Init/MPI_Finalize inside
+// and cannot); every call rebuilds from the input (a fresh GaussPyInit + GenerateDoG), i.e. what
+// one reference call produces.  Errors abort with a message instead of continuing.
+#ifndef SIFT_GAUSSDEPYRAMID_HIP_MPI_H
+#define SIFT_GAUSSDEPYRAMID_HIP_MPI_H
+
+#include <mpi.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+
+#include "gdp.h"
+#include "gdp_comm.h"
+
+class GaussPyramid_hip_mpi {
+public:
+    int** data;
+    GaussPyramid_hip_mpi();
+    GaussPyramid_hip_mpi(int** img, int len, int S);
+    float**** GaussPy;
+    void GaussPyInit();
+    void output();
+    void GaussFilter(int theLayer);
+    void GenerateDoG();
+    void GenerateDoG_mpi_normal() {}  // empty in the reference (:337-339)
+    void GenerateDoG_mpi(int argc, char** argv);
+    ~GaussPyramid_hip_mpi();
+    int thread_count;  // kept for source compatibility (:39-43); unused on the GPU
+    int chunk_size;
+    int all_time;
+    int rank() const { return rank_; }
+
+protected:
+    int length;
+    int S;
+    int layer;
+    float* filter;
+    bool is_initialized;
+    gdp_ctx* full_;  // whole-image context: single-process methods and the collector's target
+    gdp_ctx* band_;
+    gdp_comm* comm_;
+    int rank_, size_;
+    bool owns_mpi_;
+    // the error text is read only after the failing call returned (never as a sibling argument,
+    // whose evaluation order relative to the call is unspecified)
+    static void check_(int status, const char* what, const gdp_ctx* c) {
+        if (status != GDP_OK) {
+            std::fprintf(stderr, "GaussPyramid_hip_mpi::%s failed: %s (%s)\n", what, gdp_status_string(status),
+                         gdp_last_error(c));
+            std::abort();
+        }
+    }
+    static void check_comm_(int status, const char* what, const gdp_comm* c) {
+        if (status != GDP_OK) {
+            std::fprintf(stderr, "GaussPyramid_hip_mpi::%s failed: %s (%s)\n", what, gdp_status_string(status),
+                         gdp_comm_last_error(c));
+            std::abort();
+        }
+    }
+    void sync_host_() {
+        for (int o = 0; o < layer; ++o)
+            for (int s = 0; s < S + 3; ++s)
+                check_(gdp_download_level_rows(full_, 0, o, s, GaussPy[o][s]), "download", full_);
+    }
+};
+
+inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi()
+    : data(nullptr), GaussPy(nullptr), thread_count(8), chunk_size(5), all_time(0), length(0), S(0), layer(0),
+      filter(nullptr), is_initialized(false), full_(nullptr), band_(nullptr), comm_(nullptr), rank_(0), size_(1),
+      owns_mpi_(false) {}
+
+inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi(int** img, int len, int S_) : GaussPyramid_hip_mpi() {
+    length = len;
+    S = S_;
+    data = new int*[len];
+    for (int i = 0; i < len; ++i) {
+        data[i] = new int[len];
+        for (int j = 0; j < len; ++j) data[i][j] = img[i][j];
+    }
+    layer = gdp_octaves_for(len);
+    filter = new float[len];
+    GaussPy = new float***[layer];
+    for (int o = 0; o < layer; ++o) {
+        GaussPy[o] = new float**[S + 3];
+        for (int s = 0; s < S + 3; ++s) {
+            GaussPy[o][s] = new float*[len >> o];
+            for (int r = 0; r < (len >> o); ++r) GaussPy[o][s][r] = new float[len >> o];
+        }
+    }
+    GaussPyInit();
+}
+
+// The rank this process will have, also before MPI_Init (main.cpp constructs the pyramid before
+// its first GenerateDoG_mpi call): MPI_Comm_rank when MPI is up, else the launcher's environment.
+inline int gdp_launcher_rank() {
+    int on = 0;
+    MPI_Initialized(&on);
+    if (on) {
+        int r = 0;
+        MPI_Comm_rank(MPI_COMM_WORLD, &r);
+        return r;
+    }
+    for (const char* v : {"PMI_RANK", "OMPI_COMM_WORLD_RANK", "PMIX_RANK", "SLURM_PROCID", "RANK"})
+        if (const char* e = std::getenv(v)) return std::atoi(e);
+    return 0;
+}
+
+inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GPU)
+    if (!full_) {
+        const int ndev = gdp_device_count();
+        check_(gdp_create(&full_, length, length, S, layer, 1, ndev > 0 ? gdp_launcher_rank() % ndev : 0),
+               "GaussPyInit", nullptr);
+        check_(gdp_set_input_rows(full_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit", full_);
+    }
+    check_(gdp_init(full_, nullptr), "GaussPyInit", full_);
+    is_initialized = true;
+    sync_host_();
+}
+
+inline void GaussPyramid_hip_mpi::GaussFilter(int theLayer) {  // :133-167
+    check_(gdp_gauss_octave(full_, theLayer, nullptr), "GaussFilter", full_);
+    sync_host_();
+}
+
+inline void GaussPyramid_hip_mpi::GenerateDoG() {  // :169-183 (single process, current contents)
+    check_(gdp_generate_dog(full_, nullptr), "GenerateDoG", full_);
+    sync_host_();
+}
+
+inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :265-335
+    int inited = 0;
+    MPI_Initialized(&inited);
+    if (!inited) {
+        MPI_Init(&argc, &argv);
+        owns_mpi_ = true;
+    }
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank_);
+    MPI_Comm_size(MPI_COMM_WORLD, &size_);
+    const int ndev = gdp_device_count();
+    const int device = ndev > 0 ? rank_ % ndev : 0;
+    if (!comm_) {
+        unsigned char id[GDP_COMM_ID_BYTES] = {0};
+        if (rank_ == 0) check_comm_(gdp_comm_unique_id(id), "GenerateDoG_mpi", nullptr);
+        MPI_Bcast(id, GDP_COMM_ID_BYTES, MPI_BYTE, 0, MPI_COMM_WORLD);
+        check_comm_(gdp_comm_init(&comm_, id, size_, rank_, device), "GenerateDoG_mpi", nullptr);
+        int r0, r1;
+        check_comm_(gdp_band_rows(length, size_, rank_, layer, &r0, &r1), "GenerateDoG_mpi", nullptr);
+        if (r1 > r0) {  // more ranks than aligned bands leaves the last ranks without rows
+            check_(gdp_create_band(&band_, length, length, S, layer, 1, r0, r1, device), "GenerateDoG_mpi",
+                   nullptr);
+            check_(gdp_set_input_rows(band_, 0, (const int32_t* const*)(data + r0), nullptr), "GenerateDoG_mpi",
+                   band_);
+        }
+    }
+    if (band_) check_(gdp_build(band_, nullptr), "GenerateDoG_mpi", band_);
+    check_comm_(gdp_comm_gather_bands(comm_, band_, 0, rank_ == 0 ? full_ : nullptr, 0, 0, nullptr), "GenerateDoG_mpi",
+                comm_);
+    if (rank_ == 0) sync_host_();
+}
+
+inline void GaussPyramid_hip_mpi::output() {  // :116-131
+    int len = length;
+    for (int i = 0; i < layer; ++i) {
+        for (int j = 0; j < len; ++j) {
+            for (int k = 0; k < len; ++k) std::cout << GaussPy[i][0][j][k] << " ";
+            std::cout << std::endl;
+        }
+        for (int k = 0; k < len; ++k) std::cout << "==";
+        std::cout << std::endl;
+        len /= 2;
+    }
+}
+
+inline GaussPyramid_hip_mpi::~GaussPyramid_hip_mpi() {
+    if (GaussPy) {
+        for (int o = 0; o < layer; ++o) {
+            for (int s = 0; s < S + 3; ++s) {
+                for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
+                delete[] GaussPy[o][s];
+            }
+            delete[] GaussPy[o];
+        }
+        delete[] GaussPy;
+    }
+    if (data) {
+        for (int i = 0; i < length; ++i) delete[] data[i];
+        delete[] data;
+    }
+    delete[] filter;
+    gdp_comm_destroy(comm_);
+    gdp_destroy(band_);
+    gdp_destroy(full_);
+    if (owns_mpi_) {
+        int fin = 0;
+        MPI_Finalized(&fin);
+        if (!fin) MPI_Finalize();
+    }
+}
+
+#endif  // SIFT_GAUSSDEPYRAMID_HIP_MPI_H

@@ -58,6 +58,9 @@ enum {
 #define GDP_ABI_VERSION 1
 int gdp_abi_version(void);
 
+/* Number of visible HIP devices (0 when none / no driver). */
+int gdp_device_count(void);
+
 /* Number of octaves the reference builds for an n-pixel axis: floor(log2 n) + 1
  * (GaussPyramid ctor, GuassDePyramid.h:48-53). */
 int gdp_octaves_for(int n);

@@ -1,0 +1,51 @@
+/*
+ * gdp_comm.h — C ABI of libgdp_comm.so: the multi-GPU collector over RCCL (xGMI).
+ *
+ * The RCCL counterpart of the reference's MPI collector (GaussPyramid_mpi::GenerateDoG_mpi,
+ * GaussDePyramid-MPI.h:265-335: ranks < S+3 filter one scale each and MPI_Send every row to rank
+ * S+3, which receives them, :295-303, and forms all DoG levels, :304-318).  Here every rank builds
+ * one ROW BAND of the whole pyramid on its own GPU (gdp_create_band; DoG fused, any world size)
+ * and the collector receives each band's finished levels straight into a whole-image context with
+ * RCCL point-to-point transfers — one grouped send per level instead of one MPI_Send per row.
+ *
+ * Bootstrap is the caller's: rank 0 calls gdp_comm_unique_id and broadcasts the 128 bytes with
+ * whatever launcher it has (MPI_Bcast in include/GaussDePyramid-HIP-mpi.h), then every rank calls
+ * gdp_comm_init.  Uses only the public gdp.h ABI of the contexts it is given.
+ */
+#ifndef GDP_COMM_H_
+#define GDP_COMM_H_
+
+#include "gdp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gdp_comm gdp_comm;
+#define GDP_COMM_ID_BYTES 128
+
+/* Rows [row_begin, row_end) of rank `rank`'s band of an H-row image split over `nranks` ranks:
+ * multiples of 2^(max(octaves,5)-1), the last band ends at H (what gdp_create_band accepts). */
+int gdp_band_rows(int height, int nranks, int rank, int octaves, int* row_begin, int* row_end);
+
+int gdp_comm_unique_id(unsigned char id[GDP_COMM_ID_BYTES]);
+int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int nranks, int rank, int device);
+void gdp_comm_destroy(gdp_comm* comm);
+int gdp_comm_rank(const gdp_comm* comm);
+int gdp_comm_size(const gdp_comm* comm);
+const char* gdp_comm_last_error(const gdp_comm* comm); /* comm may be NULL: last init failure */
+
+/* Collective over all ranks of `comm`: every rank passes its band context (built with
+ * gdp_band_rows' rows of the same H, W, S, octaves) and image index `band_image`; rank `root`
+ * also passes `full`, a whole-image context of the same geometry, whose image `full_image`
+ * receives every band's levels (other ranks pass NULL).  A non-root rank whose band is empty
+ * (more ranks than aligned bands) passes band = NULL and returns at once.  Stream-ordered on `stream` (NULL = the
+ * band context's stream); blocking until the transfers are complete on return. */
+int gdp_comm_gather_bands(gdp_comm* comm, gdp_ctx* band, int band_image, gdp_ctx* full, int full_image, int root,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDP_COMM_H_ */

@@ -40,6 +40,7 @@ _pp = ctypes.POINTER(ctypes.c_void_p)
 SIGNATURES = {
     "gdp_abi_version": (_c_int, []),
     "gdp_octaves_for": (_c_int, [_c_int]),
+    "gdp_device_count": (_c_int, []),
     "gdp_create": (_c_int, [_pp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
     "gdp_create_band": (_c_int, [_pp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
     "gdp_destroy": (None, [_p]),

@@ -706,6 +706,11 @@ int gdp_abi_version(void) { return GDP_ABI_VERSION; }
 
 int gdp_octaves_for(int n) { return octaves_for(n); }
 
+int gdp_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 const char* gdp_status_string(int s) {
     switch (s) {
         case GDP_OK: return "ok";

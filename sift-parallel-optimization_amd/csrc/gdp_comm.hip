@@ -1,0 +1,176 @@
+// libgdp_comm.so — RCCL collector for row-band pyramids (include/gdp_comm.h).
+// Host-only code (no kernels): RCCL grouped point-to-point transfers of finished band levels
+// into the collector's whole-image context, plus the band arithmetic shared with bench.py /
+// distributed.py (plan_band, band_level_rows).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "gdp_comm.h"
+
+struct gdp_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0, device = 0;
+    std::string err;
+};
+
+namespace {
+thread_local std::string g_comm_error;
+
+int fail(gdp_comm* c, int code, const std::string& m) {
+    if (c)
+        c->err = m;
+    else
+        g_comm_error = m;
+    return code;
+}
+
+#define GDP_NCCL(c, call)                                                                                 \
+    do {                                                                                                  \
+        ncclResult_t r_ = (call);                                                                         \
+        if (r_ != ncclSuccess) return fail((c), GDP_ERR_HIP, std::string(#call ": ") + ncclGetErrorString(r_)); \
+    } while (0)
+#define GDP_HIPC(c, call)                                                                                 \
+    do {                                                                                                  \
+        hipError_t e_ = (call);                                                                           \
+        if (e_ != hipSuccess) return fail((c), GDP_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+int band_align(int octaves) { return 1 << (std::max(octaves, 5) - 1); }
+
+// (first global row, rows) of octave o for the band [r0, r1) of an H-row image — gdp_level_dims
+// of a band context, computed for any rank without its context.
+void band_level(int H, int o, int r0, int r1, int* first, int* rows) {
+    const int Hg = H >> o;
+    *first = (r0 + (1 << o) - 1) >> o;
+    const int hi = (r1 == H) ? Hg : std::min(Hg, (r1 + (1 << o) - 1) >> o);
+    *rows = std::max(0, hi - *first);
+}
+}  // namespace
+
+extern "C" {
+
+int gdp_band_rows(int H, int nranks, int rank, int octaves, int* row_begin, int* row_end) {
+    if (H <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || octaves <= 0 || !row_begin || !row_end)
+        return GDP_ERR_ARG;
+    // per = ceil(ceil(H / nranks) / align) * align — distributed.plan_band, same numbers
+    const long long align = band_align(octaves);
+    const long long hn = ((long long)H + nranks - 1) / nranks;
+    const long long per = (hn + align - 1) / align * align;
+    *row_begin = (int)std::min<long long>(H, (long long)rank * per);
+    *row_end = (int)std::min<long long>(H, (long long)(rank + 1) * per);
+    return GDP_OK;
+}
+
+int gdp_comm_unique_id(unsigned char id[GDP_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == GDP_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(nullptr, GDP_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(id, &u, sizeof u);
+    return GDP_OK;
+}
+
+int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int nranks, int rank, int device) {
+    if (!out || !id || nranks <= 0 || rank < 0 || rank >= nranks) return fail(nullptr, GDP_ERR_ARG, "gdp_comm_init: bad argument");
+    *out = nullptr;
+    gdp_comm* c = new (std::nothrow) gdp_comm();
+    if (!c) return fail(nullptr, GDP_ERR_NOMEM, "host allocation failed");
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(nullptr, GDP_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(nullptr, GDP_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    *out = c;
+    return GDP_OK;
+}
+
+void gdp_comm_destroy(gdp_comm* c) {
+    if (!c) return;
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+}
+
+int gdp_comm_rank(const gdp_comm* c) { return c ? c->rank : -1; }
+int gdp_comm_size(const gdp_comm* c) { return c ? c->nranks : -1; }
+const char* gdp_comm_last_error(const gdp_comm* c) { return c ? c->err.c_str() : g_comm_error.c_str(); }
+
+int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* full, int full_image, int root,
+                          void* stream) {
+    // band == NULL: this rank's band is empty (more ranks than aligned row bands); it sends nothing
+    if (!c || root < 0 || root >= c->nranks || (c->rank == root && !full) || (!band && c->rank == root && !full))
+        return fail(c, GDP_ERR_ARG, "gdp_comm_gather_bands: bad argument");
+    int H, W, S, O, B;
+    if (gdp_get_geometry(band ? band : full, &H, &W, &S, &O, &B) != GDP_OK) {
+        if (band || c->rank == root) return fail(c, GDP_ERR_ARG, "band geometry");
+    }
+    if (c->rank == root) {
+        int H2, W2, S2, O2, B2;
+        gdp_get_geometry(full, &H2, &W2, &S2, &O2, &B2);
+        int rows0, cols0, first0;
+        gdp_level_dims(full, 0, &rows0, &cols0, &first0);
+        if (H2 != H || W2 != W || S2 != S || O2 != O || first0 != 0 || rows0 != H)
+            return fail(c, GDP_ERR_ARG, "collector context must be the whole image of the same geometry");
+    }
+    GDP_HIPC(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)gdp_stream(band ? band : full);
+    if (!band && c->rank != root) return GDP_OK;  // empty band: nothing to send, nothing to receive
+    const int L = S + 3;
+    GDP_NCCL(c, ncclGroupStart());
+    if (c->rank != root) {
+        for (int o = 0; o < O; ++o) {
+            int rows, cols, first;
+            gdp_level_dims(band, o, &rows, &cols, &first);
+            for (int s = 0; s < L && rows > 0; ++s)
+                GDP_NCCL(c, ncclSend(gdp_device_level(band, band_image, o, s), (size_t)rows * cols, ncclFloat, root,
+                                     c->comm, st));
+        }
+    } else {
+        for (int r = 0; r < c->nranks; ++r) {
+            if (r == root) continue;
+            int r0, r1;
+            gdp_band_rows(H, c->nranks, r, O, &r0, &r1);
+            for (int o = 0; o < O; ++o) {
+                int first, rows;
+                band_level(H, o, r0, r1, &first, &rows);
+                const int cols = W >> o;
+                for (int s = 0; s < L && rows > 0; ++s) {
+                    float* dst = const_cast<float*>(gdp_device_level(full, full_image, o, s)) + (size_t)first * cols;
+                    GDP_NCCL(c, ncclRecv(dst, (size_t)rows * cols, ncclFloat, r, c->comm, st));
+                }
+            }
+        }
+    }
+    GDP_NCCL(c, ncclGroupEnd());
+    if (c->rank == root && band) {  // the collector's own band: device-to-device copies
+        for (int o = 0; o < O; ++o) {
+            int rows, cols, first;
+            gdp_level_dims(band, o, &rows, &cols, &first);
+            for (int s = 0; s < L && rows > 0; ++s) {
+                float* dst = const_cast<float*>(gdp_device_level(full, full_image, o, s)) + (size_t)first * cols;
+                GDP_HIPC(c, hipMemcpyAsync(dst, gdp_device_level(band, band_image, o, s), (size_t)rows * cols * 4,
+                                           hipMemcpyDeviceToDevice, st));
+            }
+        }
+    }
+    GDP_HIPC(c, hipStreamSynchronize(st));
+    return GDP_OK;
+}
+
+}  // extern "C"

@@ -158,6 +158,8 @@ def _gpu_band_compute(H, W, S, O, device):
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
 
     def compute(img_band, r0, r1):
+        if r1 <= r0:  # more ranks than aligned bands: this rank holds no rows
+            return torch.empty(0, dtype=torch.float32, device=dev)
         with PyramidContext(H, W, S=S, octaves=O, batch=1, device=dev.index, row_begin=r0, row_end=r1) as ctx:
             out = torch.empty(ctx.pyramid_bytes() // 4 + 64, dtype=torch.float32, device=dev)
             base = out.data_ptr()

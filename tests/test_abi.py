@@ -86,3 +86,34 @@ def test_product_never_reaches_the_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 text = open(os.path.join(root, f)).read()
                 assert "liboracle" not in text and "gdp_oracle" not in text and "load_oracle" not in text, f
+
+
+def _comm_lib():
+    import ctypes
+
+    path = os.path.join(PKG, "lib", "libgdp_comm.so")
+    assert os.path.exists(path)
+    return ctypes.CDLL(path)
+
+
+def test_comm_library_exports_its_header(pkg):
+    pkg.lib()  # torch first, then libgdp (the comm library links both)
+    L = _comm_lib()
+    names = pkg.header_functions(os.path.join(REPO, "include", "gdp_comm.h"))
+    assert len(names) == 8
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_band_rows_match_the_python_plan(pkg):
+    """gdp_band_rows (C++ collector) and distributed.plan_band (Python driver) split identically."""
+    import ctypes
+    import importlib
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    L = _comm_lib()
+    r0, r1 = ctypes.c_int(), ctypes.c_int()
+    for H, world, O in [(16384, 8, 5), (97, 3, 5), (100, 2, 7), (4096, 7, 13), (1080, 4, 5), (512, 6, 10), (33, 8, 5)]:
+        for r in range(world):
+            assert L.gdp_band_rows(H, world, r, O, ctypes.byref(r0), ctypes.byref(r1)) == 0
+            assert (r0.value, r1.value) == d.plan_band(H, world, r, O), (H, world, O, r)

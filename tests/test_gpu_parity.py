@@ -456,3 +456,29 @@ def test_cpp_mpitest_dropin_matches_oracle(oracle, tmp_path):
         assert float(r.stdout.split()[0]) >= 0  # elapsed seconds, printed like the collector rank
         _assert_same(np.fromfile(out, dtype=np.float32), oracle.build_pyramid(oracle.image_from_spec(n, spec), 2),
                      ("mpitest", n, spec))
+
+
+def test_cpp_mpi_variant_dropin_collector(oracle, golden, tmp_path):
+    """GaussPyramid_hip_mpi (GaussDePyramid-MPI.h's class, MPI as launcher + RCCL collector):
+    the collector's GaussPy after GenerateDoG_mpi == the reference, as an MPI singleton and under
+    mpiexec -n 1 (one GPU on the box; ranks > 1 need one GPU each — RCCL rejects two ranks on
+    one device)."""
+    exe = os.path.join(REPO, "examples", "mpi_hip")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not os.path.exists(exe):
+        pytest.skip("examples/mpi_hip not built (no MPI headers at build time)")
+    rec = [r for r in golden["hashes"] if r["n"] == 512 and r["input"] == "lcg:12345"][0]
+    out = tmp_path / "c.f32"
+    cmds = [[exe, "512", "lcg:12345", str(out)]]
+    if os.path.exists(mpiexec):
+        cmds.append([mpiexec, "-n", "1", exe, "512", "lcg:12345", str(out)])
+    for cmd in cmds:
+        if out.exists():
+            out.unlink()
+        subprocess.run(cmd, check=True, timeout=180, capture_output=True)
+        lv = oracle.levels(np.fromfile(out, dtype=np.float32), 512, 512, 2, 10)
+        for o, row in enumerate(rec["octaves"]):
+            for s, h in enumerate(row):
+                assert oracle.fnv(lv[(o, s)]) == int(h, 16), (cmd[0], o, s)
+    subprocess.run([exe, "100", "lcg:3", str(out)], check=True, timeout=180, capture_output=True)
+    _assert_same(np.fromfile(out, dtype=np.float32), oracle.build_pyramid(oracle.lcg_image(100, 100, 3), 2), "mpi 100")
