@@ -178,9 +178,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
                     help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
-    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss"],
+    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv"],
                     help="build: fused GaussPyInit+GenerateDoG (headline); regen: in-place GenerateDoG "
-                         "re-entry; gauss: in-place row+column window pass of every octave")
+                         "re-entry; gauss: in-place row+column window pass of every octave; conv: the "
+                         "true-Gaussian-convolution extension (not the reference's algorithm)")
     args = ap.parse_args()
 
     import torch
@@ -233,6 +234,8 @@ def main():
 
     if args.op == "build":
         step = ctx.build
+    elif args.op == "conv":
+        step = ctx.build_gaussian
     else:
         ctx.build(stream)  # materialise the pyramid the in-place passes work on
         step = ctx.generate_dog if args.op == "regen" else (lambda st: ctx.gauss_range(0, O, st))
@@ -262,7 +265,7 @@ def main():
     rows_local = ctx.row_end - ctx.row_begin
     in_bytes = 1 if args.input == "u8" else 4
     pyr_px = sum(ctx.level_dims(o)[0] * ctx.level_dims(o)[1] for o in range(O)) * (1 if cfg["band"] else B)
-    if args.op != "build":  # in-place passes read and write every level once: 8*(S+3)*P bytes
+    if args.op not in ("build", "conv"):  # in-place passes read and write every level once: 8*(S+3)*P bytes
         bytes_launch = 8 * (S + 3) * pyr_px
     elif cfg["band"]:
         bytes_launch = in_bytes * rows_local * W + 4 * (S + 3) * pyr_px
@@ -298,14 +301,16 @@ def main():
             "kernel": ("k_build (fused decimate+window+DoG), variant %d" % ctx.tuning()["variant"]
                        if args.op == "build" else
                        {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
-                        "gauss": "k_levels<MODE=1> (in-place row+column window, all octaves)"}[args.op]),
+                        "gauss": "k_window (in-place row+column window, all octaves)",
+                        "conv": "k_conv (extension: separable Gaussian convolution, LDS halo tiles)"}[args.op]),
             "kernel_ms": round(kernel_ms, 6),
             "algorithmic_bytes_per_launch": bytes_launch,
         },
     }
     result["parity"] = parity if args.op == "build" else {"status": "not checked for in-place re-entry ops"}
     if args.op != "build":
-        result["metric"] = METRIC + f" [op={args.op}: in-place pass]"
+        result["metric"] = METRIC + (" [op=conv: true-Gaussian extension, not the reference's algorithm]"
+                                     if args.op == "conv" else f" [op={args.op}: in-place pass]")
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
     elif rank == 0:

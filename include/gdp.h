@@ -132,6 +132,15 @@ int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);
  * like the reference's repeated-call timing loop (main.cpp:66-73). */
 int gdp_generate_dog(gdp_ctx* ctx, void* stream);
 
+/* ---- extension: true Gaussian convolution pyramid --------------------------
+ * NOT the reference's algorithm (which multiplies by a window, :119-131) and carries no parity
+ * claim: G_s = base_o (*) k_s, the separable Gaussian with sigma_s = 2/(s+1) (the reference's
+ * schedule), normalised taps over radius ceil(3 sigma_s) (<= 6), clamp-to-edge borders; same octave
+ * bases, DoG and level layout as gdp_build.  Whole-image contexts only (a band has no halo rows).
+ * gdp_conv_taps returns scale s's 13 taps (zero beyond 2R+1) and radius R. */
+int gdp_build_gaussian(gdp_ctx* ctx, void* stream);
+int gdp_conv_taps(int S, int scale, float* taps13, int* radius);
+
 /* ---- output --------------------------------------------------------------------------------
  * The blocking copies below are ordered after work on the context's OWN stream; if a build was
  * launched on another stream, synchronize that stream first. */

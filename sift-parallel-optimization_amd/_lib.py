@@ -56,6 +56,8 @@ SIGNATURES = {
     "gdp_set_input_device_u8": (_c_int, [_p, _p, _c_size, _c_size]),
     "gdp_fill_synthetic": (_c_int, [_p, _c_u32, _c_long, _p]),
     "gdp_build": (_c_int, [_p, _p]),
+    "gdp_build_gaussian": (_c_int, [_p, _p]),
+    "gdp_conv_taps": (_c_int, [_c_int, _c_int, _p, ctypes.POINTER(_c_int)]),
     "gdp_init": (_c_int, [_p, _p]),
     "gdp_gauss_octave": (_c_int, [_p, _c_int, _p]),
     "gdp_gauss_range": (_c_int, [_p, _c_int, _c_int, _p]),

@@ -89,6 +89,8 @@ struct Geom {
     unsigned tail_groups_per_img, tail_units;  // octaves >= F, 256 groups per unit
     OctGeom oct[kMaxOct];
     unsigned lv_blk[kMaxOct + 1]; // prefix over octaves of ceil(rows*gpr / kLevBlock) per image
+    unsigned cv_blk[kMaxOct + 1]; // convolution mode: prefix over octaves of 16x256 output tiles
+    int cv_tiles_c[kMaxOct];      // convolution mode: tile columns per octave
 };
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -477,6 +479,133 @@ __global__ void __launch_bounds__(kLevBlock) k_window(const Geom* __restrict__ g
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Extension (no reference counterpart, no parity claim): a TRUE separable
+// Gaussian convolution pyramid.  Same octave bases (decimated input) and σ schedule
+// (σ_s = sigma/(s+1)) and the same DoG layout as the reference, but G_s = base ⊛ k_s with
+// normalised taps over radius R_s = ceil(3σ_s) and clamp-to-edge borders.  This is the stencil the
+// north star's "LDS halo" design is for: each block stages its 16 x 256 output tile plus a 6-pixel
+// halo of the base image in LDS once, then for every scale runs the horizontal pass LDS -> LDS
+// and the vertical pass LDS -> registers, forms the DoG against the previous scale in registers
+// and streams the S+3 levels out with 1-KiB wave stores.
+// ------------------------------------------------------------------------------------------
+constexpr int kCvTH = 16, kCvTW = 256;  // output tile
+constexpr int kCvR = 6;                 // max radius: ceil(3 * sigma_0) with sigma_0 = 2
+constexpr int kCvPadL = 8;              // left halo (16-B aligned rows)
+constexpr int kCvInW = kCvTW + 2 * kCvPadL;
+constexpr int kCvInH = kCvTH + 2 * kCvR;
+constexpr int kCvMaxTaps = 2 * kCvR + 1;
+
+template <int R>
+__device__ __forceinline__ void conv_h_row(const float* __restrict__ in_row, float* __restrict__ h_row, int cg,
+                                           const float* __restrict__ k) {
+    // outputs at tile cols 4cg..4cg+3 <- LDS in cols kCvPadL + 4cg - R .. kCvPadL + 4cg + 3 + R
+    float w[4 + 2 * R];
+    const float* src = in_row + kCvPadL + 4 * cg - R;
+#pragma unroll
+    for (int j = 0; j < 4 + 2 * R; ++j) w[j] = src[j];
+    f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d <= 2 * R; ++d) {
+        const float kd = k[d];
+        o.x += kd * w[d];
+        o.y += kd * w[d + 1];
+        o.z += kd * w[d + 2];
+        o.w += kd * w[d + 3];
+    }
+    *reinterpret_cast<f4*>(h_row + 4 * cg) = o;
+}
+
+template <int R>
+__device__ __forceinline__ void conv_pass(const float* __restrict__ in_s, float* __restrict__ h_s, const float* k,
+                                          int tid, f4 (&g)[4]) {
+    // horizontal pass: LDS rows kCvR-R .. kCvR+kCvTH+R-1, 64 column groups per row
+    const int nrows = kCvTH + 2 * R;
+    for (int item = tid; item < nrows * 64; item += 256) {
+        const int i = kCvR - R + item / 64;
+        conv_h_row<R>(in_s + i * kCvInW, h_s + i * kCvTW, item & 63, k);
+    }
+    __syncthreads();
+    // vertical pass: thread (rg, cg) owns output rows 4rg..4rg+3, columns 4cg..4cg+3
+    const int cg = tid & 63, rg = tid >> 6;
+    f4 w[4 + 2 * R];
+#pragma unroll
+    for (int j = 0; j < 4 + 2 * R; ++j) w[j] = *reinterpret_cast<const f4*>(h_s + (kCvR + 4 * rg - R + j) * kCvTW + 4 * cg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int d = 0; d <= 2 * R; ++d) o += k[d] * w[q + d];
+        g[q] = o;
+    }
+    __syncthreads(); // h_s is rewritten by the next scale
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256, 2) k_conv(const Geom* __restrict__ g, const void* __restrict__ in,
+                                                 float* __restrict__ out, const float* __restrict__ ctaps,
+                                                 const int* __restrict__ cradius) {
+    __shared__ __attribute__((aligned(16))) float in_s[kCvInH * kCvInW];
+    __shared__ __attribute__((aligned(16))) float h_s[kCvInH * kCvTW];
+    const unsigned per = g->cv_blk[g->O];
+    const unsigned b = blockIdx.x / per;
+    const unsigned v = blockIdx.x - b * per;
+    int o = 0;
+    while (o + 1 < g->O && v >= g->cv_blk[o + 1]) ++o;
+    const OctGeom og = g->oct[o];
+    const unsigned t = v - g->cv_blk[o];
+    const int tr = (int)(t / (unsigned)g->cv_tiles_c[o]);
+    const int tc = (int)(t - (unsigned)tr * (unsigned)g->cv_tiles_c[o]);
+    const int r0 = tr * kCvTH, c0 = tc * kCvTW; // octave-o output coordinates of the tile
+    const int tid = threadIdx.x;
+    const int rows = og.rows, cols = og.cols;
+    // stage the base-image tile + halo (clamp-to-edge), decimated from the input, as float
+    const long long img_off = (long long)b * g->in_img_stride;
+    for (int e = tid; e < kCvInH * kCvInW; e += 256) {
+        const int i = e / kCvInW, j = e - (e / kCvInW) * kCvInW;
+        const int r = min(max(r0 - kCvR + i, 0), rows - 1);
+        const int c = min(max(c0 - kCvPadL + j, 0), cols - 1);
+        const long long idx = img_off + ((long long)r << o) * g->in_pitch + ((long long)c << o);
+        in_s[e] = g->in_fmt == GDP_INPUT_U8 ? (float)static_cast<const unsigned char*>(in)[idx]
+                                            : (float)static_cast<const int*>(in)[idx];
+    }
+    __syncthreads();
+    const int cg = tid & 63, rg = tid >> 6;
+    const int C = c0 + 4 * cg;
+    const int n = min(4, cols - C);
+    const bool full = (n == 4) && ((cols & 3) == 0);
+    float* base = out + (long long)b * g->pyr_stride + og.lev_off + C;
+    auto store = [&](int s, int q, f4 val) {
+        const int R = r0 + 4 * rg + q;
+        if (R >= rows || n <= 0) return;
+        float* p = base + (long long)s * og.lev_stride + (long long)R * cols;
+        if (full)
+            st_f4<NT>(p, val);
+        else
+            st_part(p, val, n, false);
+    };
+    f4 prev[4], cur[4];
+    for (int s = 0; s < g->L; ++s) {
+        const float* k = ctaps + s * kCvMaxTaps;
+        switch (cradius[s]) {
+            case 1: conv_pass<1>(in_s, h_s, k, tid, cur); break;
+            case 2: conv_pass<2>(in_s, h_s, k, tid, cur); break;
+            case 3: conv_pass<3>(in_s, h_s, k, tid, cur); break;
+            case 4: conv_pass<4>(in_s, h_s, k, tid, cur); break;
+            case 5: conv_pass<5>(in_s, h_s, k, tid, cur); break;
+            default: conv_pass<6>(in_s, h_s, k, tid, cur); break;
+        }
+        if (s > 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) store(s - 1, q, prev[q] - cur[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) prev[q] = cur[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) store(g->L - 1, q, prev[q]);
+}
+
 // Order-independent pyramid checksum (verification of multi-GPU runs without moving pyramids):
 // sum over every word of every level of splitmix64(global element index * phi + level id * c
 // + float bits), mod 2^64.  Global rows make row-band checksums add up to the whole image's.
@@ -592,6 +721,8 @@ struct gdp_ctx {
     const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
     float* d_taps = nullptr;
+    float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
+    int* d_cradius = nullptr;     // convolution-mode radius per scale
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
     float* h_stage = nullptr;     // pinned staging for row-pointer downloads (largest level)
     size_t h_stage_floats = 0;
@@ -800,6 +931,8 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         make_magic((unsigned)std::max(1, og.gpr), &og.gpr_magic, &og.gpr_shift);
         grp += (long long)og.rows * og.gpr;
         g.lv_blk[o + 1] = g.lv_blk[o] + (unsigned)(((long long)og.rows * og.gpr + kLevBlock - 1) / kLevBlock);
+        g.cv_tiles_c[o] = (og.cols + kCvTW - 1) / kCvTW;
+        g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
     g.pyr_stride = round_up(lev_off, kLevelAlign);
     const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
@@ -868,6 +1001,8 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_taps) (void)hipFree(c->d_taps);
     if (c->d_in_own) (void)hipFree(c->d_in_own);
     if (c->d_out_own) (void)hipFree(c->d_out_own);
+    if (c->d_ctaps) (void)hipFree(c->d_ctaps);
+    if (c->d_cradius) (void)hipFree(c->d_cradius);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->d_sum) (void)hipFree(c->d_sum);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1004,6 +1139,41 @@ int gdp_build(gdp_ctx* c, void* stream) {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_build(c, c->pick(stream));
+}
+
+int gdp_conv_taps(int S, int scale, float* taps, int* radius) {
+    if (S < 0 || scale < 0 || scale >= S + 3 || !taps || !radius) return GDP_ERR_ARG;
+    const double sig = (double)kSigma / (scale + 1);
+    const int R = std::min(kCvR, std::max(1, (int)std::ceil(3.0 * sig)));
+    double w[kCvMaxTaps], sum = 0;
+    for (int d = -R; d <= R; ++d) sum += (w[d + R] = std::exp(-(double)d * d / (2.0 * sig * sig)));
+    for (int j = 0; j < kCvMaxTaps; ++j) taps[j] = j <= 2 * R ? (float)(w[j] / sum) : 0.0f;
+    *radius = R;
+    return GDP_OK;
+}
+
+int gdp_build_gaussian(gdp_ctx* c, void* stream) {
+    if (!c) return GDP_ERR_ARG;
+    const Geom& g = c->geom;
+    if (g.in_row0 != 0 || g.in_rows != g.H)
+        return c->status(GDP_ERR_STATE, "gdp_build_gaussian: row-band contexts are not supported (needs halo rows)");
+    GDP_HIP(c, hipSetDevice(c->device));
+    if (!c->d_ctaps) {
+        std::vector<float> t((size_t)g.L * kCvMaxTaps);
+        std::vector<int> r(g.L);
+        for (int s = 0; s < g.L; ++s) gdp_conv_taps(g.S, s, t.data() + (size_t)s * kCvMaxTaps, &r[s]);
+        GDP_HIP(c, hipMalloc(&c->d_ctaps, t.size() * 4));
+        GDP_HIP(c, hipMalloc(&c->d_cradius, r.size() * 4));
+        GDP_HIP(c, hipMemcpy(c->d_ctaps, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        GDP_HIP(c, hipMemcpy(c->d_cradius, r.data(), r.size() * 4, hipMemcpyHostToDevice));
+    }
+    const long long grid = (long long)g.cv_blk[g.O] * g.batch;
+    if (grid <= 0) return GDP_OK;
+    if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
+    hipLaunchKernelGGL(c->nontemporal ? k_conv<true> : k_conv<false>, dim3((unsigned)grid), dim3(256), 0, c->pick(stream),
+                       c->d_geom, c->d_in, c->d_out, c->d_ctaps, c->d_cradius);
+    GDP_HIP(c, hipGetLastError());
+    return GDP_OK;
 }
 
 int gdp_init(gdp_ctx* c, void* stream) {

@@ -52,6 +52,14 @@ def octaves_for(n):
     return lib().gdp_octaves_for(int(n))
 
 
+def conv_taps(S, scale):
+    """(taps[0:2R+1], R) of the convolution-mode Gaussian of `scale` (gdp_conv_taps)."""
+    t = np.zeros(13, np.float32)
+    r = _i()
+    check(lib().gdp_conv_taps(int(S), int(scale), _ptr(t), ctypes.byref(r)))
+    return t[:2 * r.value + 1].copy(), r.value
+
+
 class PyramidContext:
     """`batch` images of H x W int32 (or the row band [row_begin, row_end)) on one GPU.
 
@@ -144,6 +152,10 @@ class PyramidContext:
     def build(self, stream=None):
         """Fused GaussPyInit + GenerateDoG of every image (one launch)."""
         check(lib().gdp_build(self._ctx, _stream_handle(stream)), self._ctx)
+
+    def build_gaussian(self, stream=None):
+        """Extension (no reference counterpart): true separable Gaussian convolution pyramid."""
+        check(lib().gdp_build_gaussian(self._ctx, _stream_handle(stream)), self._ctx)
 
     def init(self, stream=None):
         check(lib().gdp_init(self._ctx, _stream_handle(stream)), self._ctx)

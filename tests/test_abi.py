@@ -5,6 +5,7 @@ import ctypes
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -117,3 +118,16 @@ def test_band_rows_match_the_python_plan(pkg):
         for r in range(world):
             assert L.gdp_band_rows(H, world, r, O, ctypes.byref(r0), ctypes.byref(r1)) == 0
             assert (r0.value, r1.value) == d.plan_band(H, world, r, O), (H, world, O, r)
+
+
+def test_conv_taps_of_the_extension_mode(pkg):
+    """Host-only: normalised Gaussian taps, radius ceil(3 sigma_s) with sigma_s = 2/(s+1), <= 6."""
+    import math
+
+    for S in (0, 2, 5):
+        for s in range(S + 3):
+            k, R = pkg.conv_taps(S, s)
+            sig = 2.0 / (s + 1)
+            assert R == min(6, max(1, math.ceil(3 * sig)))
+            assert len(k) == 2 * R + 1 and abs(float(k.astype(np.float64).sum()) - 1) < 1e-6
+            assert np.allclose(k, k[::-1]) and int(np.argmax(k)) == R

@@ -482,3 +482,44 @@ def test_cpp_mpi_variant_dropin_collector(oracle, golden, tmp_path):
                 assert oracle.fnv(lv[(o, s)]) == int(h, 16), (cmd[0], o, s)
     subprocess.run([exe, "100", "lcg:3", str(out)], check=True, timeout=180, capture_output=True)
     _assert_same(np.fromfile(out, dtype=np.float32), oracle.build_pyramid(oracle.lcg_image(100, 100, 3), 2), "mpi 100")
+
+
+# ------------------------------------------------------------------ extension: true Gaussian convolution
+def _conv_reference(pkg, img, S, O):
+    """float64 numpy separable convolution with the library's taps, clamp-to-edge borders."""
+    H, W = img.shape
+    out = {}
+    for o in range(O):
+        base = img[:: 1 << o, :: 1 << o][: H >> o, : W >> o].astype(np.float64)
+        G = []
+        for s in range(S + 3):
+            k, R = pkg.conv_taps(S, s)
+            k = k.astype(np.float64)
+            p = np.pad(base, R, mode="edge")                                      # (h+2R, w+2R)
+            h = sum(k[d] * p[:, d:d + base.shape[1]] for d in range(2 * R + 1))    # rows keep the halo
+            v = sum(k[d] * h[d:d + base.shape[0]] for d in range(2 * R + 1))
+            G.append(v)
+        for s in range(S + 3):
+            out[(o, s)] = G[s] - G[s + 1] if s < S + 2 else G[s]
+    return out
+
+
+@pytest.mark.parametrize("H,W,S,O,fmt", [(64, 96, 2, 0, "i32"), (300, 500, 3, 5, "i32"), (1080, 1920, 2, 5, "u8"),
+                                          (17, 33, 1, 0, "i32")])
+def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt):
+    """Extension mode (no reference counterpart; parity unpinned by construction): checked against
+    a float64 separable convolution.  Tolerance: |gpu - ref| <= 1e-3 + 1e-5 |ref| (float32
+    accumulation of <= 13 taps on pixels <= 255)."""
+    img = oracle.lcg_image(H, W, 21)
+    if fmt == "u8":
+        img = img.astype(np.uint8)
+    with pkg.PyramidContext(H, W, S=S, octaves=O, input_format=fmt) as ctx:
+        ctx.set_input(img)
+        ctx.build_gaussian()
+        ctx.sync()
+        want = _conv_reference(pkg, img.astype(np.int32), S, ctx.O)
+        for (o, s), ref in want.items():
+            got = ctx.level(0, o, s).astype(np.float64)
+            assert got.shape == ref.shape
+            err = np.abs(got - ref) - (1e-3 + 1e-5 * np.abs(ref))
+            assert err.max() <= 0, ((o, s), float(np.abs(got - ref).max()))

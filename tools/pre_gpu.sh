@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Build everything and run the CPU suite; used as `tools/pre_gpu.sh && gpurun ...`.
-set -e
+set -eo pipefail
 cd "$(dirname "$0")/.."
 python -c "import __graft_entry__ as g; g.build()"
 make -s -C tools membench 2>/dev/null || true
