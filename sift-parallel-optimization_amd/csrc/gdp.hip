@@ -496,57 +496,83 @@ constexpr int kCvInW = kCvTW + 2 * kCvPadL;
 constexpr int kCvInH = kCvTH + 2 * kCvR;
 constexpr int kCvMaxTaps = 2 * kCvR + 1;
 
+// No bit-exactness contract in this mode, so the stencil uses fused multiply-adds explicitly
+// (the file-wide contract(off) keeps the reference path unfused).
+__device__ __forceinline__ f4 fma4(float k, f4 x, f4 acc) {
+    const f4 kk = {k, k, k, k};
+    return __builtin_elementwise_fma(kk, x, acc);
+}
+
+// Vertical pass first (rows of the staged tile carry the vertical halo): h_s[r][j] for the 16 output
+// rows and all kCvInW staged columns (the horizontal halo included), one float4 column group and
+// four rows per work item, the 4 + 2R input rows read once per item.
 template <int R>
-__device__ __forceinline__ void conv_h_row(const float* __restrict__ in_row, float* __restrict__ h_row, int cg,
-                                           const float* __restrict__ k) {
-    // outputs at tile cols 4cg..4cg+3 <- LDS in cols kCvPadL + 4cg - R .. kCvPadL + 4cg + 3 + R
-    float w[4 + 2 * R];
-    const float* src = in_row + kCvPadL + 4 * cg - R;
+__device__ __forceinline__ void conv_v_pass(const float* __restrict__ in_s, float* __restrict__ h_s, const float* k,
+                                            int tid) {
+    // 2 x 68 items of 8 rows x 4 columns: one iteration for threads 0..135 (the 272-column staged
+    // width is not a multiple of 256 lanes, so 4-row items would give one wave two iterations)
+    constexpr int kG = kCvInW / 4; // float4 column groups per staged row
+    constexpr int kRows = kCvTH / 2;
+    if (tid >= 2 * kG) return;
+    const int rq = tid / kG, j4 = tid - (tid / kG) * kG;
+    f4 w[kRows + 2 * R];
 #pragma unroll
-    for (int j = 0; j < 4 + 2 * R; ++j) w[j] = src[j];
-    f4 o = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < kRows + 2 * R; ++j)
+        w[j] = *reinterpret_cast<const f4*>(in_s + (kCvR - R + kRows * rq + j) * kCvInW + 4 * j4);
 #pragma unroll
-    for (int d = 0; d <= 2 * R; ++d) {
-        const float kd = k[d];
-        o.x += kd * w[d];
-        o.y += kd * w[d + 1];
-        o.z += kd * w[d + 2];
-        o.w += kd * w[d + 3];
+    for (int q = 0; q < kRows; ++q) {
+        f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int d = 0; d <= 2 * R; ++d) o = fma4(k[d], w[q + d], o);
+        *reinterpret_cast<f4*>(h_s + (kRows * rq + q) * kCvInW + 4 * j4) = o;
     }
-    *reinterpret_cast<f4*>(h_row + 4 * cg) = o;
+}
+
+// Horizontal pass: thread (rg, cg) produces output rows 4rg..4rg+3, columns 4cg..4cg+3, reading
+// the aligned float4s that cover staged columns kCvPadL + 4cg - R .. kCvPadL + 4cg + 3 + R.
+template <int R>
+__device__ __forceinline__ void conv_h_pass(const float* __restrict__ h_s, const float* k, int tid, f4 (&g)[4]) {
+    constexpr int kLo = (kCvPadL - R) / 4 * 4;
+    constexpr int kN = (kCvPadL + 4 + R - kLo + 3) / 4;
+    const int cg = tid & 63, rg = tid >> 6;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float a[4 * kN];
+        const float* src = h_s + (4 * rg + q) * kCvInW + 4 * cg + kLo;
+#pragma unroll
+        for (int j = 0; j < kN; ++j) {
+            const f4 v = *reinterpret_cast<const f4*>(src + 4 * j);
+            a[4 * j] = v.x;
+            a[4 * j + 1] = v.y;
+            a[4 * j + 2] = v.z;
+            a[4 * j + 3] = v.w;
+        }
+        const float* w = a + (kCvPadL - R - kLo);
+        f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int d = 0; d <= 2 * R; ++d) {
+            const f4 x = {w[d], w[d + 1], w[d + 2], w[d + 3]};
+            o = fma4(k[d], x, o);
+        }
+        g[q] = o;
+    }
 }
 
 template <int R>
 __device__ __forceinline__ void conv_pass(const float* __restrict__ in_s, float* __restrict__ h_s, const float* k,
                                           int tid, f4 (&g)[4]) {
-    // horizontal pass: LDS rows kCvR-R .. kCvR+kCvTH+R-1, 64 column groups per row
-    const int nrows = kCvTH + 2 * R;
-    for (int item = tid; item < nrows * 64; item += 256) {
-        const int i = kCvR - R + item / 64;
-        conv_h_row<R>(in_s + i * kCvInW, h_s + i * kCvTW, item & 63, k);
-    }
+    conv_v_pass<R>(in_s, h_s, k, tid);
     __syncthreads();
-    // vertical pass: thread (rg, cg) owns output rows 4rg..4rg+3, columns 4cg..4cg+3
-    const int cg = tid & 63, rg = tid >> 6;
-    f4 w[4 + 2 * R];
-#pragma unroll
-    for (int j = 0; j < 4 + 2 * R; ++j) w[j] = *reinterpret_cast<const f4*>(h_s + (kCvR + 4 * rg - R + j) * kCvTW + 4 * cg);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        f4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int d = 0; d <= 2 * R; ++d) o += k[d] * w[q + d];
-        g[q] = o;
-    }
+    conv_h_pass<R>(h_s, k, tid, g);
     __syncthreads(); // h_s is rewritten by the next scale
 }
 
 template <bool NT>
-__global__ void __launch_bounds__(256, 2) k_conv(const Geom* __restrict__ g, const void* __restrict__ in,
+__global__ void __launch_bounds__(256, 3) k_conv(const Geom* __restrict__ g, const void* __restrict__ in,
                                                  float* __restrict__ out, const float* __restrict__ ctaps,
                                                  const int* __restrict__ cradius) {
     __shared__ __attribute__((aligned(16))) float in_s[kCvInH * kCvInW];
-    __shared__ __attribute__((aligned(16))) float h_s[kCvInH * kCvTW];
+    __shared__ __attribute__((aligned(16))) float h_s[kCvTH * kCvInW];
     const unsigned per = g->cv_blk[g->O];
     const unsigned b = blockIdx.x / per;
     const unsigned v = blockIdx.x - b * per;
@@ -561,6 +587,25 @@ __global__ void __launch_bounds__(256, 2) k_conv(const Geom* __restrict__ g, con
     const int rows = og.rows, cols = og.cols;
     // stage the base-image tile + halo (clamp-to-edge), decimated from the input, as float
     const long long img_off = (long long)b * g->in_img_stride;
+    const bool interior = o == 0 && g->vec_in && g->in_fmt == GDP_INPUT_I32 && r0 - kCvR >= 0 &&
+                          r0 + kCvTH + kCvR <= rows && c0 - kCvPadL >= 0 && c0 + kCvTW + kCvPadL <= cols;
+    if (interior) {  // no clamping: 16-B int4 loads (all issued first), 16-B LDS stores
+        const int* src = static_cast<const int*>(in) + img_off + (long long)(r0 - kCvR) * g->in_pitch + (c0 - kCvPadL);
+        constexpr int kItems = kCvInH * (kCvInW / 4);
+        constexpr int kIter = (kItems + 255) / 256;
+        i4 v[kIter];
+#pragma unroll
+        for (int u = 0; u < kIter; ++u) {
+            const int e = tid + 256 * u;
+            const int i = e / (kCvInW / 4), j4 = e - i * (kCvInW / 4);
+            if (e < kItems) v[u] = *reinterpret_cast<const i4*>(src + (long long)i * g->in_pitch + 4 * j4);
+        }
+#pragma unroll
+        for (int u = 0; u < kIter; ++u) {
+            const int e = tid + 256 * u;
+            if (e < kItems) *reinterpret_cast<f4*>(in_s + 4 * e) = __builtin_convertvector(v[u], f4);
+        }
+    } else
     for (int e = tid; e < kCvInH * kCvInW; e += 256) {
         const int i = e / kCvInW, j = e - (e / kCvInW) * kCvInW;
         const int r = min(max(r0 - kCvR + i, 0), rows - 1);
