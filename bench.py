@@ -176,6 +176,11 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override images per GPU")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--variant", type=int, default=None,
+                    help="force a build-kernel variant (and skip autotuning), e.g. for profiling runs")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
+                         "variant on this device before the warm-up; all variants give identical bits)")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
                     help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv"],
@@ -232,6 +237,11 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
+    autotuned = None
+    if args.variant is not None:
+        ctx.set_tuning(variant=args.variant)
+    elif args.op == "build" and not args.no_autotune:
+        autotuned = ctx.autotune(iters=3 if B * H * W > (1 << 28) else 10, stream=stream)
     if args.op == "build":
         step = ctx.build
     elif args.op == "conv":
@@ -298,7 +308,8 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(pmc["kernel_bytes_per_launch"]) if pmc else None,
-            "kernel": ("k_build (fused decimate+window+DoG), variant %d" % ctx.tuning()["variant"]
+            "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d%s"
+                       % (ctx.tuning()["variant"], ctx.tuning()["tile_order"], " (autotuned)" if autotuned else "")
                        if args.op == "build" else
                        {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
                         "gauss": "k_window (in-place row+column window, all octaves)",

@@ -181,12 +181,19 @@ enum {
     GDP_TUNE_BLOCKS_PER_CU = 2, /* value > 0: persistent build grid = CUs x value;
                                    0 (default): one 16x256 tile per block                      */
     GDP_TUNE_GRID = 3,          /* explicit build grid size; 0 (default) = automatic         */
-    GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile width), 0..6;
+    GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile shape), 0..8;
                                    default chosen from the image width                         */
-    GDP_TUNE_TILE_ORDER = 5     /* build tile order: 0 linear (default), 1 XCD-chunked,
+    GDP_TUNE_TILE_ORDER = 5,    /* build tile order: 0 linear (default), 1 XCD-chunked,
                                    2 XCD row-interleaved                                       */
+    GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk
+                                   (1 default, 2 or 4)                                         */
+    GDP_TUNE_WINDOW_SUB = 7     /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
+/* Benchmark every build-kernel variant x tile order on the context's current input (`iters`
+ * launches each, HIP events on `stream`) and keep the fastest; reports the choice and its
+ * per-launch ms.  Results are bit-identical for every candidate.  Overwrites the pyramid. */
+int gdp_autotune(gdp_ctx* ctx, int iters, void* stream, int* variant, int* tile_order, float* ms_per_build);
 int gdp_get_tuning(const gdp_ctx* ctx, int key, int* value);
 
 /* ---- misc ---------------------------------------------------------------------------------- */

@@ -21,6 +21,7 @@ HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "gdp.h")
 GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV = range(6)
 GDP_INPUT_I32, GDP_INPUT_U8 = 0, 1
 GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT, GDP_TUNE_TILE_ORDER = 1, 2, 3, 4, 5
+GDP_TUNE_INPLACE_SUB, GDP_TUNE_WINDOW_SUB = 6, 7
 
 
 class GdpError(RuntimeError):
@@ -79,6 +80,8 @@ SIGNATURES = {
     "gdp_status_string": (ctypes.c_char_p, [_c_int]),
     "gdp_time_builds": (_c_int, [_p, _c_int, _p, ctypes.POINTER(ctypes.c_float)]),
     "gdp_set_tuning": (_c_int, [_p, _c_int, _c_int]),
+    "gdp_autotune": (_c_int, [_p, _c_int, _p, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
+                              ctypes.POINTER(ctypes.c_float)]),
     "gdp_get_tuning": (_c_int, [_p, _c_int, ctypes.POINTER(_c_int)]),
 }
 

@@ -254,7 +254,7 @@ __device__ __forceinline__ void tile_octave0(const Geom* __restrict__ g, const v
 // octaves >= F.  Default launch: one unit per block (the dispatcher back-fills CUs as blocks
 // retire, which measured faster than a persistent grid); the grid-stride loop serves capped grids.
 // BLK = threads per block; O0REG selects the register-resident octave-0 path (BLK = 256 only).
-template <int LT, bool NT, int BLK, int TC, bool O0REG>
+template <int LT, bool NT, int BLK, int TC, bool O0REG, int TR>
 __device__ __forceinline__ void build_body(const Geom* __restrict__ g, const void* __restrict__ in,
                                            float* __restrict__ out, const float* __restrict__ taps) {
     const unsigned tiles_total = g->tiles_total;
@@ -278,12 +278,13 @@ __device__ __forceinline__ void build_body(const Geom* __restrict__ g, const voi
             const unsigned rem = t - b * g->tiles_per_img;
             const unsigned tr = rem / (unsigned)g->tiles_c;
             const unsigned tc = rem - tr * (unsigned)g->tiles_c;
-            const int in_r0 = (int)tr * kTileRows; // band-local input row of the tile
+            const int in_r0 = (int)tr * TR; // band-local input row of the tile
             const int in_c0 = (int)tc * TC;
+            constexpr int kFusedT = TR == 16 ? 5 : TR == 8 ? 4 : TR == 4 ? 3 : TR == 2 ? 2 : 1; // log2(TR)+1
 #pragma unroll
-            for (int o = 0; o < kFused; ++o) {
+            for (int o = 0; o < kFusedT; ++o) {
                 if (o >= F) break;
-                if constexpr (LT > 0 && O0REG && BLK == 256 && TC == kTileCols) {
+                if constexpr (LT > 0 && O0REG && BLK == 256 && TC == kTileCols && TR == kTileRows) {
                     if (o == 0) {
                         tile_octave0<LT, NT>(g, in, out, taps, (int)b, in_r0, in_c0);
                         continue;
@@ -291,7 +292,7 @@ __device__ __forceinline__ void build_body(const Geom* __restrict__ g, const voi
                 }
                 const OctGeom og = g->oct[o];
                 const int gpr_t = (TC / 4) >> o; // groups per tile row (TC = 256: 64, 32, 16, 8, 4)
-                const int groups = (kTileRows >> o) * gpr_t;
+                const int groups = (TR >> o) * gpr_t;
 #pragma unroll
                 for (int q0 = 0; q0 < groups; q0 += BLK) {
                     const int q = q0 + (int)threadIdx.x;
@@ -324,39 +325,44 @@ __device__ __forceinline__ void build_body(const Geom* __restrict__ g, const voi
     }
 }
 
-template <int LT, bool NT, int BLK, int TC, bool O0REG>
+template <int LT, bool NT, int BLK, int TC, bool O0REG, int TR>
 __global__ void __launch_bounds__(BLK) k_build(const Geom* __restrict__ g, const void* __restrict__ in,
                                                float* __restrict__ out, const float* __restrict__ taps) {
-    build_body<LT, NT, BLK, TC, O0REG>(g, in, out, taps);
+    build_body<LT, NT, BLK, TC, O0REG, TR>(g, in, out, taps);
 }
 
 // Build-kernel code variants (GDP_TUNE_VARIANT); all bit-identical, A/B'd by tools/tune.py.
 struct BuildVariant {
-    int block, tile_cols;
+    int block, tile_cols, tile_rows;
     void (*k[2][2])(const Geom*, const void*, float*, const float*); // [LT==5][NT]
 };
-#define GDP_VARIANT(BLK, TC, REG)                                                                \
-    BuildVariant {                                                                               \
-        BLK, TC, {{k_build<0, false, BLK, TC, REG>, k_build<0, true, BLK, TC, REG>},              \
-                  {k_build<5, false, BLK, TC, REG>, k_build<5, true, BLK, TC, REG>}}              \
+#define GDP_VARIANT(BLK, TC, REG, TR)                                                             \
+    BuildVariant {                                                                                \
+        BLK, TC, TR, {{k_build<0, false, BLK, TC, REG, TR>, k_build<0, true, BLK, TC, REG, TR>},   \
+                      {k_build<5, false, BLK, TC, REG, TR>, k_build<5, true, BLK, TC, REG, TR>}}   \
     }
 const BuildVariant kVariants[] = {
-    GDP_VARIANT(1024, 256, false), // 0 (default): 16 waves, one octave-0 group per thread
-    GDP_VARIANT(256, 256, true),   // 1: 4 waves, register-resident octave 0 (4 groups per thread)
-    GDP_VARIANT(512, 256, false),  // 2: 8 waves, 2 groups per thread
-    GDP_VARIANT(256, 256, false),  // 3: 4 waves, generic loop
-    GDP_VARIANT(512, 128, false),  // 4: 8 waves, 16 x 128 tile, one group per thread
-    GDP_VARIANT(1024, 512, false), // 5: 16 waves, 16 x 512 tile, 2 groups per thread
-    GDP_VARIANT(256, 64, false),   // 6: 4 waves, 16 x 64 tile, one group per thread
+    GDP_VARIANT(1024, 256, false, 16), // 0 (default): 16 waves, one octave-0 group per thread
+    GDP_VARIANT(256, 256, true, 16),   // 1: 4 waves, register-resident octave 0 (4 groups per thread)
+    GDP_VARIANT(512, 256, false, 16),  // 2: 8 waves, 2 groups per thread
+    GDP_VARIANT(256, 256, false, 16),  // 3: 4 waves, generic loop
+    GDP_VARIANT(512, 128, false, 16),  // 4: 8 waves, 16 x 128 tile, one group per thread
+    GDP_VARIANT(1024, 512, false, 16), // 5: 16 waves, 16 x 512 tile, 2 groups per thread
+    GDP_VARIANT(256, 64, false, 16),   // 6: 4 waves, 16 x 64 tile, one group per thread
+    GDP_VARIANT(256, 256, false, 4),   // 7: 4 waves, 4 x 256 tile (octaves 0-2 fused, 3+ as tail units)
+    GDP_VARIANT(512, 256, false, 8),   // 8: 8 waves, 8 x 256 tile (octaves 0-3 fused)
 };
 
 // Default variant for a width (tools/tune.py, MI355X): 1024 threads on 16 x 256 tiles (v0) is the
 // fastest everywhere the width fills its tiles; when a 256-wide tile grid would leave more lanes
 // idle than a 128-wide one (e.g. W = 1920: 7.5 tiles), 512 threads on 16 x 128 tiles (v4).
-int default_variant(int W) {
+// A single image of <= 16 Mpix (e.g. the 4096^2 headline) is fastest on 8 x 256 tiles with 512
+// threads (v8: 0.067 vs 0.073 ms at 4096^2); batches stream best with v0.  gdp_autotune measures.
+int default_variant(int W, long long pixels, int batch) {
     const long long waste256 = (long long)((W + 255) / 256) * 256 - W;
     const long long waste128 = (long long)((W + 127) / 128) * 128 - W;
-    return waste256 * 128 > waste128 * 256 ? 4 : 0;
+    if (waste256 * 128 > waste128 * 256) return 4;
+    return (batch == 1 && pixels <= (1ll << 24)) ? 8 : 0;
 }
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -365,18 +371,20 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 // 4 = refill from the input (GaussPyInit; exclusive).  One block = kLevBlock consecutive groups
 // (4 pixels each) of one octave's level rows; every thread owns one group across all S+3 levels:
 // the S+3 float4 loads are issued together (LT known), then the rolling window/DoG and the stores.
-template <int LT, int MODE, bool NT>
-__global__ void __launch_bounds__(kLevBlock) k_levels(const Geom* __restrict__ g, const void* __restrict__ in,
-                                                      float* __restrict__ out, const float* __restrict__ taps,
-                                                      int o_begin, int o_end) {
+// SUB splits each 1024-group chunk over SUB blocks of 1024/SUB threads (GDP_TUNE_INPLACE_SUB).
+template <int LT, int MODE, bool NT, int SUB>
+__global__ void __launch_bounds__(kLevBlock / SUB) k_levels(const Geom* __restrict__ g, const void* __restrict__ in,
+                                                            float* __restrict__ out, const float* __restrict__ taps,
+                                                            int o_begin, int o_end) {
     const unsigned first = g->lv_blk[o_begin];
     const unsigned per = g->lv_blk[o_end] - first;
-    const unsigned b = blockIdx.x / per;
-    const unsigned v = blockIdx.x - b * per + first;
+    const unsigned chunk = blockIdx.x / SUB;
+    const unsigned b = chunk / per;
+    const unsigned v = chunk - b * per + first;
     int o = o_begin;
     while (o + 1 < o_end && v >= g->lv_blk[o + 1]) ++o;
     const OctGeom og = g->oct[o];
-    const unsigned k = (v - g->lv_blk[o]) * kLevBlock + threadIdx.x;
+    const unsigned k = (v - g->lv_blk[o]) * kLevBlock + (blockIdx.x % SUB) * (kLevBlock / SUB) + threadIdx.x;
     if (k >= (unsigned)og.rows * (unsigned)og.gpr) return;
     const int Rl = (int)fast_div(k, og.gpr_magic, og.gpr_shift);
     const int C = 4 * (int)(k - (unsigned)Rl * (unsigned)og.gpr);
@@ -445,21 +453,22 @@ __global__ void __launch_bounds__(kLevBlock) k_levels(const Geom* __restrict__ g
 // an octave are independent under the window, so every thread moves exactly one float4 (load,
 // two multiplies, store) — the shape that streams best in place on MI355X (tools/membench:
 // 1 float4 per lane with non-temporal load+store ≈ 6.5 TB/s vs ≈ 6.1 at 4 per lane).
-template <bool NT>
-__global__ void __launch_bounds__(kLevBlock) k_window(const Geom* __restrict__ g, float* __restrict__ out,
-                                                      const float* __restrict__ taps, int o_begin, int o_end) {
+template <bool NT, int SUB>
+__global__ void __launch_bounds__(kLevBlock / SUB) k_window(const Geom* __restrict__ g, float* __restrict__ out,
+                                                            const float* __restrict__ taps, int o_begin, int o_end) {
     const unsigned L = (unsigned)g->L;
     const unsigned first = g->lv_blk[o_begin] * L;
     const unsigned per = g->lv_blk[o_end] * L - first;
-    const unsigned b = blockIdx.x / per;
-    const unsigned v = blockIdx.x - b * per + first;
+    const unsigned chunk = blockIdx.x / SUB;
+    const unsigned b = chunk / per;
+    const unsigned v = chunk - b * per + first;
     int o = o_begin;
     while (o + 1 < o_end && v >= g->lv_blk[o + 1] * L) ++o;
     const OctGeom og = g->oct[o];
     const unsigned nb = g->lv_blk[o + 1] - g->lv_blk[o]; // blocks per level of octave o
     const unsigned w = v - g->lv_blk[o] * L;
     const int s = (int)(w / nb);
-    const unsigned k = (w - (unsigned)s * nb) * kLevBlock + threadIdx.x;
+    const unsigned k = (w - (unsigned)s * nb) * kLevBlock + (blockIdx.x % SUB) * (kLevBlock / SUB) + threadIdx.x;
     if (k >= (unsigned)og.rows * (unsigned)og.gpr) return;
     const int Rl = (int)fast_div(k, og.gpr_magic, og.gpr_shift);
     const int C = 4 * (int)(k - (unsigned)Rl * (unsigned)og.gpr);
@@ -781,6 +790,9 @@ struct gdp_ctx {
     int grid_override = 0;        // GDP_TUNE_GRID (0 = automatic)
     int persistent = 0;           // set by GDP_TUNE_BLOCKS_PER_CU: grid = CUs x blocks per CU
     int variant = 0;              // GDP_TUNE_VARIANT: index into kVariants (default_variant(W))
+    int inplace_sub = 1;          // GDP_TUNE_INPLACE_SUB: k_levels blocks per 1024-group chunk (1, 2, 4)
+    int window_sub = 4;           // GDP_TUNE_WINDOW_SUB: k_window blocks per chunk (4 = 256-thread blocks:
+                                  // 6.7 vs 5.9 TB/s at 4096^2, tools/tune.py)
     std::string err;
     int status(int code, const char* fmt, ...) {
         char buf[512];
@@ -807,9 +819,20 @@ namespace {
     } while (0)
 
 // Tile grid of the selected build variant (tile width differs per variant).
-int retile(gdp_ctx* c, int tile_cols) {
+int retile(gdp_ctx* c, int tile_cols, int tile_rows) {
     Geom& g = c->geom;
-    g.tiles_r = (g.in_rows + kTileRows - 1) / kTileRows;
+    // octaves fused into a tile: those with whole rows in it (tile_rows = 2^(F-1)); the rest are
+    // flattened tail units
+    int fused = 1;
+    while ((1 << fused) <= tile_rows) ++fused;
+    g.F = std::min(g.O, std::min(fused, kFused));
+    const long long total_groups = g.oct[g.O - 1].grp_begin + (long long)g.oct[g.O - 1].rows * g.oct[g.O - 1].gpr;
+    const long long tail_per_img = (g.F < g.O) ? total_groups - g.oct[g.F].grp_begin : 0;
+    const long long tail_units = (tail_per_img * g.batch + kTailGroups - 1) / kTailGroups;
+    if (tail_per_img * g.batch >= (1ll << 31)) return c->status(GDP_ERR_ARG, "image/batch too large for one context");
+    g.tail_groups_per_img = (unsigned)tail_per_img;
+    g.tail_units = (unsigned)tail_units;
+    g.tiles_r = (g.in_rows + tile_rows - 1) / tile_rows;
     g.tiles_c = (g.W + tile_cols - 1) / tile_cols;
     const long long tiles_per_img = (long long)g.tiles_r * g.tiles_c;
     if (tiles_per_img * g.batch + g.tail_units >= (1ll << 31))
@@ -842,29 +865,39 @@ int launch_build(gdp_ctx* c, hipStream_t st) {
     return GDP_OK;
 }
 
-template <int MODE>
-int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
+template <int MODE, int SUB>
+int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     const Geom& g = c->geom;
     if constexpr (MODE == 1) {
-        const long long grid = ((long long)g.lv_blk[oe] - g.lv_blk[ob]) * g.L * g.batch;
+        const long long grid = ((long long)g.lv_blk[oe] - g.lv_blk[ob]) * g.L * g.batch * SUB;
         if (grid <= 0) return GDP_OK;
         if (grid >= (1ll << 31) || (long long)g.lv_blk[g.O] * g.L >= (1ll << 32))
             return c->status(GDP_ERR_ARG, "window pass too large for one launch");
-        hipLaunchKernelGGL(c->nontemporal ? k_window<true> : k_window<false>, dim3((unsigned)grid), dim3(kLevBlock), 0, st,
-                           c->d_geom, c->d_out, c->d_taps, ob, oe);
+        auto wkern = c->nontemporal ? k_window<true, SUB> : k_window<false, SUB>;
+        hipLaunchKernelGGL(wkern, dim3((unsigned)grid), dim3(kLevBlock / SUB), 0, st, c->d_geom, c->d_out, c->d_taps, ob,
+                           oe);
         GDP_HIP(c, hipGetLastError());
         return GDP_OK;
     }
     const long long per = (long long)g.lv_blk[oe] - g.lv_blk[ob];
-    const long long grid = per * g.batch;
+    const long long grid = per * g.batch * SUB;
     if (grid <= 0) return GDP_OK;
     if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "in-place pass too large for one launch");
-    auto kern = g.L == 5 ? (c->nontemporal ? k_levels<5, MODE, true> : k_levels<5, MODE, false>)
-                         : (c->nontemporal ? k_levels<0, MODE, true> : k_levels<0, MODE, false>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kLevBlock), 0, st, c->d_geom, c->d_in, c->d_out, c->d_taps, ob,
-                       oe);
+    auto kern = g.L == 5 ? (c->nontemporal ? k_levels<5, MODE, true, SUB> : k_levels<5, MODE, false, SUB>)
+                         : (c->nontemporal ? k_levels<0, MODE, true, SUB> : k_levels<0, MODE, false, SUB>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kLevBlock / SUB), 0, st, c->d_geom, c->d_in, c->d_out, c->d_taps,
+                       ob, oe);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
+}
+
+template <int MODE>
+int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
+    switch (MODE == 1 ? c->window_sub : c->inplace_sub) {
+        case 2: return launch_inplace_sub<MODE, 2>(c, ob, oe, st);
+        case 4: return launch_inplace_sub<MODE, 4>(c, ob, oe, st);
+        default: return launch_inplace_sub<MODE, 1>(c, ob, oe, st);
+    }
 }
 
 bool valid_level(const gdp_ctx* c, int b, int o, int s) {
@@ -931,7 +964,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     gdp_ctx* c = new (std::nothrow) gdp_ctx();
     if (!c) return fail(GDP_ERR_NOMEM, "host allocation failed");
     c->device = device;
-    c->variant = default_variant(W);
+    c->variant = default_variant(W, (long long)(row_end - row_begin) * W, batch);
     c->cus = std::max(1, prop.multiProcessorCount);
     c->blocks_max = c->cus * 8;
     Geom& g = c->geom;
@@ -994,7 +1027,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // 16384^2 config) streams 7-8 % faster when each XCD sweeps its own contiguous eighth of the
     // tiles; batches and <= 4096^2 images are fastest in linear order.
     g.tile_order = (batch == 1 && (long long)g.in_rows * W >= (1ll << 26)) ? 1 : 0;
-    retile(c, kVariants[c->variant].tile_cols);
+    retile(c, kVariants[c->variant].tile_cols, kVariants[c->variant].tile_rows);
     c->h_taps.assign((size_t)tap_off, 0.0f);
     for (int o = 0; o < O; ++o) {
         const OctGeom& og = g.oct[o];
@@ -1373,6 +1406,41 @@ int gdp_sync(gdp_ctx* c) {
 
 void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* best_order, float* best_ms) {
+    // Times every build-kernel variant x tile order on the context's current input (HIP events on
+    // `stream`, median of 3 repeats of `iters` launches) and keeps the fastest.  All candidates
+    // produce identical bits, so this only ever changes speed.
+    if (!c || iters <= 0) return c ? c->status(GDP_ERR_ARG, "gdp_autotune: iters must be > 0") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    const int old_variant = c->variant, old_order = c->geom.tile_order;
+    int bv = old_variant, bo = old_order;
+    float bt = 3.4e38f;
+    for (int v = 0; v < kNumVariants; ++v) {
+        for (int ord = 0; ord <= 1; ++ord) {
+            int rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, v);
+            if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, ord);
+            if (rc != GDP_OK) return rc;
+            float t[3];
+            rc = gdp_time_builds(c, 1, stream, &t[0]);  // warm-up
+            for (int r = 0; r < 3 && rc == GDP_OK; ++r) rc = gdp_time_builds(c, iters, stream, &t[r]);
+            if (rc != GDP_OK) return rc;
+            std::sort(t, t + 3);
+            if (t[1] < bt) {
+                bt = t[1];
+                bv = v;
+                bo = ord;
+            }
+        }
+    }
+    int rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, bv);
+    if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, bo);
+    if (rc != GDP_OK) return rc;
+    if (best_variant) *best_variant = bv;
+    if (best_order) *best_order = bo;
+    if (best_ms) *best_ms = bt / iters;
+    return GDP_OK;
+}
+
 int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
     if (!c || !value) return GDP_ERR_ARG;
     switch (key) {
@@ -1381,6 +1449,8 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_GRID: *value = c->grid_override; return GDP_OK;
         case GDP_TUNE_VARIANT: *value = c->variant; return GDP_OK;
         case GDP_TUNE_TILE_ORDER: *value = c->geom.tile_order; return GDP_OK;
+        case GDP_TUNE_INPLACE_SUB: *value = c->inplace_sub; return GDP_OK;
+        case GDP_TUNE_WINDOW_SUB: *value = c->window_sub; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 }
@@ -1400,6 +1470,11 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             if (value < 0) return c->status(GDP_ERR_ARG, "grid must be >= 0");
             c->grid_override = value;
             return GDP_OK;
+        case GDP_TUNE_INPLACE_SUB:
+        case GDP_TUNE_WINDOW_SUB:
+            if (value != 1 && value != 2 && value != 4) return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4");
+            (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
+            return GDP_OK;
         case GDP_TUNE_TILE_ORDER:
             if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");
             c->geom.tile_order = value;
@@ -1408,11 +1483,11 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             if (value < 0 || value >= kNumVariants) return c->status(GDP_ERR_ARG, "variant out of range");
             const int old = c->variant;
             c->variant = value;
-            int rc = retile(c, kVariants[value].tile_cols);
+            int rc = retile(c, kVariants[value].tile_cols, kVariants[value].tile_rows);
             if (rc == GDP_OK) rc = upload_geom(c);
             if (rc != GDP_OK) {
                 c->variant = old;
-                retile(c, kVariants[old].tile_cols);
+                retile(c, kVariants[old].tile_cols, kVariants[old].tile_rows);
             }
             return rc;
         }

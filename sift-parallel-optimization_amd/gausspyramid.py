@@ -181,24 +181,35 @@ class PyramidContext:
     def stream(self):
         return lib().gdp_stream(self._ctx)
 
-    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None):
-        """Performance knobs of the build kernel (outputs are bit-identical for every setting)."""
-        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_TILE_ORDER,
-                           GDP_TUNE_VARIANT)
+    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None,
+                   inplace_sub=None, window_sub=None):
+        """Performance knobs of the kernels (outputs are bit-identical for every setting)."""
+        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_INPLACE_SUB, GDP_TUNE_NONTEMPORAL,
+                           GDP_TUNE_TILE_ORDER, GDP_TUNE_VARIANT, GDP_TUNE_WINDOW_SUB)
 
         for key, val in ((GDP_TUNE_NONTEMPORAL, nontemporal), (GDP_TUNE_BLOCKS_PER_CU, blocks_per_cu),
-                         (GDP_TUNE_GRID, grid), (GDP_TUNE_VARIANT, variant), (GDP_TUNE_TILE_ORDER, tile_order)):
+                         (GDP_TUNE_GRID, grid), (GDP_TUNE_VARIANT, variant), (GDP_TUNE_TILE_ORDER, tile_order),
+                         (GDP_TUNE_INPLACE_SUB, inplace_sub), (GDP_TUNE_WINDOW_SUB, window_sub)):
             if val is not None:
                 check(lib().gdp_set_tuning(self._ctx, key, int(val)), self._ctx)
 
+    def autotune(self, iters=5, stream=None):
+        """Time every build variant x tile order on the current input and keep the fastest;
+        returns (variant, tile_order, ms per build).  Overwrites the pyramid (bits unchanged)."""
+        v, o, ms = _i(), _i(), ctypes.c_float()
+        check(lib().gdp_autotune(self._ctx, int(iters), _stream_handle(stream), ctypes.byref(v), ctypes.byref(o),
+                                 ctypes.byref(ms)), self._ctx)
+        return v.value, o.value, ms.value
+
     def tuning(self):
         """Current {nontemporal, blocks_per_cu, grid, variant} of the build kernel."""
-        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_NONTEMPORAL, GDP_TUNE_TILE_ORDER,
-                           GDP_TUNE_VARIANT)
+        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_INPLACE_SUB, GDP_TUNE_NONTEMPORAL,
+                           GDP_TUNE_TILE_ORDER, GDP_TUNE_VARIANT, GDP_TUNE_WINDOW_SUB)
 
         out = {}
         for name, key in (("nontemporal", GDP_TUNE_NONTEMPORAL), ("blocks_per_cu", GDP_TUNE_BLOCKS_PER_CU),
-                          ("grid", GDP_TUNE_GRID), ("variant", GDP_TUNE_VARIANT), ("tile_order", GDP_TUNE_TILE_ORDER)):
+                          ("grid", GDP_TUNE_GRID), ("variant", GDP_TUNE_VARIANT), ("tile_order", GDP_TUNE_TILE_ORDER),
+                          ("inplace_sub", GDP_TUNE_INPLACE_SUB), ("window_sub", GDP_TUNE_WINDOW_SUB)):
             v = _i()
             check(lib().gdp_get_tuning(self._ctx, key, ctypes.byref(v)), self._ctx)
             out[name] = v.value

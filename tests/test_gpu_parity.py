@@ -112,7 +112,7 @@ def test_build_matches_oracle_shapes(pkg, oracle, H, W, S, O):
     _assert_same(_gpu_pyramid(pkg, img, S, O), want, (H, W, S, O))
 
 
-@pytest.mark.parametrize("variant", range(7))
+@pytest.mark.parametrize("variant", range(9))
 def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
     """Every code variant of the build kernel (block size / tile width / octave-0 path, also
     persistent grids and plain stores) produces identical bits."""
@@ -128,9 +128,21 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
                 _assert_same(ctx.pyramid(0), want, (variant, H, W, S, O, kw))
 
 
-def test_default_variant_follows_width(pkg):
-    with pkg.PyramidContext(64, 4096, S=2) as a, pkg.PyramidContext(64, 1920, S=2) as b:
-        assert a.tuning()["variant"] == 0 and b.tuning()["variant"] == 4
+def test_default_variant_follows_geometry(pkg):
+    with pkg.PyramidContext(64, 4096, S=2, batch=2) as a, pkg.PyramidContext(64, 1920, S=2) as b, \
+            pkg.PyramidContext(4096, 4096, S=2, octaves=5) as c:
+        assert a.tuning()["variant"] == 0 and b.tuning()["variant"] == 4 and c.tuning()["variant"] == 8
+
+
+def test_autotune_keeps_results_bit_exact(pkg, oracle):
+    img = oracle.lcg_image(300, 512, 6)
+    with pkg.PyramidContext(300, 512, S=2, octaves=5) as ctx:
+        ctx.set_input(img)
+        v, o, ms = ctx.autotune(iters=2)
+        assert 0 <= v <= 8 and o in (0, 1) and ms > 0
+        assert ctx.tuning()["variant"] == v and ctx.tuning()["tile_order"] == o
+        ctx.build()
+        _assert_same(ctx.pyramid(0), oracle.build_pyramid(img, 2, 5), ("autotuned", v, o))
 
 
 def test_large_value_and_negative_inputs(pkg, oracle):
@@ -264,15 +276,15 @@ def test_inplace_ops_match_reference_order(pkg, oracle):
         _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
 
 
-@pytest.mark.parametrize("nt", [1, 0])
-def test_gauss_range_and_store_modes(pkg, oracle, nt):
+@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4)])
+def test_gauss_range_and_store_modes(pkg, oracle, nt, sub):
     """One-launch GaussFilter over an octave range == per-octave GaussFilter; both store modes;
     a batch of 3 and a generic-S (S = 4) context."""
     for H, W, S, B in [(90, 200, 2, 3), (64, 48, 4, 1)]:
         O = oracle.default_octaves(H, W)
         imgs = [oracle.lcg_image(H, W, 5 + b) for b in range(B)]
         with pkg.PyramidContext(H, W, S=S, batch=B) as ctx:
-            ctx.set_tuning(nontemporal=nt)
+            ctx.set_tuning(nontemporal=nt, inplace_sub=sub, window_sub=4 // sub)
             for b, img in enumerate(imgs):
                 ctx.set_input(img, b)
             ctx.init()

@@ -41,7 +41,7 @@ def main():
         kv = dict(p.split("=") for p in v.split(","))
         variants.append((v, {"nontemporal": int(kv.get("nt", 1)), "grid": int(kv.get("grid", "0"), 0),
                              "variant": int(kv.get("v", -1)) if "v" in kv else None,
-                             "tile_order": int(kv.get("ord", 0))}))
+                             "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1))}))
         if variants[-1][1]["variant"] is None:
             del variants[-1][1]["variant"]
         if "bpc" in kv:
