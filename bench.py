@@ -135,7 +135,8 @@ def latest_pmc(config_key):
                         rec = json.load(fh)
                 except (OSError, ValueError):
                     continue
-                if rec.get("config") == config_key and rec.get("kernel_bytes_per_launch"):
+                if rec.get("config") == config_key and rec.get("op", "build") == "build" and \
+                        rec.get("kernel_bytes_per_launch"):
                     best = rec
     return best
 

@@ -23,14 +23,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-KERNEL = "k_build"
 
 
-def counter_values(path, counter):
+def counter_values(path, counter, name):
     vals = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if r["Kernel_Name"] == name and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -43,23 +42,29 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--round", default="r01")
     ap.add_argument("--bench-json", help="bench.py output line of the traced run (optional)")
+    ap.add_argument("--kernel", default="k_build", help="substring of the kernel to summarise")
+    ap.add_argument("--op", default="build", help="bench.py --op of the profiled run")
     args = ap.parse_args()
 
     import bench
 
-    stats = None
+    stats = None  # the timed kernel: the matching row with the most calls
     with open(os.path.join(args.trace, "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
-            if KERNEL in r["Name"]:
+            if args.kernel in r["Name"] and (stats is None or int(r["Calls"]) > int(stats["Calls"])):
                 stats = r
-    fetch = counter_values(os.path.join(args.fetch, "run_counter_collection.csv"), "FETCH_SIZE")
-    write = counter_values(os.path.join(args.write, "run_counter_collection.csv"), "WRITE_SIZE")
+    name = stats["Name"]
+    fetch = counter_values(os.path.join(args.fetch, "run_counter_collection.csv"), "FETCH_SIZE", name)
+    write = counter_values(os.path.join(args.write, "run_counter_collection.csv"), "WRITE_SIZE", name)
     cfg = bench.CONFIGS[args.config]
-    alg = bench.algorithmic_bytes(cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"])
+    if args.op == "build":
+        alg = bench.algorithmic_bytes(cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"])
+    else:  # in-place passes read and write every level: 8*(S+3)*P
+        alg = 8 * 5 * cfg["batch"] * bench.pyramid_pixels(cfg["H"], cfg["W"], cfg["O"])
     read_b = 2 * statistics.median(fetch) * 1024
     write_b = statistics.median(write) * 1024
     rec = {
-        "config": args.config, "round": args.round, "kernel": stats["Name"] if stats else KERNEL,
+        "config": args.config, "round": args.round, "kernel": name,
         "trace_calls": int(stats["Calls"]) if stats else None,
         "trace_avg_ns": float(stats["AverageNs"]) if stats else None,
         "trace_min_ns": float(stats["MinNs"]) if stats else None,
@@ -77,11 +82,13 @@ def main():
             for line in f:
                 if line.startswith("{"):
                     rec["bench_line_of_traced_run"] = json.loads(line)
-    out = os.path.join(HERE, f"pmc_{args.config}_{args.round}.json")
+    tag = args.config if args.op == "build" else f"{args.config}_{args.op}"
+    rec["op"] = args.op
+    out = os.path.join(HERE, f"pmc_{tag}_{args.round}.json")
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     shutil.copy(os.path.join(args.trace, "run_kernel_stats.csv"),
-                os.path.join(HERE, f"rocprof_{args.config}_{args.round}_kernel_stats.csv"))
+                os.path.join(HERE, f"rocprof_{tag}_{args.round}_kernel_stats.csv"))
     print(json.dumps(rec))
 
 
