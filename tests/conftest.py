@@ -14,6 +14,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _built():
+    """A fresh checkout has no built libraries (git-ignored): build them once (hipcc
+    cross-compiles without a GPU)."""
+    entry.ensure_built()
+
+
 @pytest.fixture(scope="session")
 def oracle():
     """The CPU checker (oracle/) — test infrastructure only."""
