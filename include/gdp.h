@@ -151,6 +151,10 @@ int gdp_download_level(gdp_ctx* ctx, int b, int octave, int scale, float* host);
 /* Copy level (o, s) of image b into host row pointers — materialises the reference's
  * float**** GaussPy[o][s] rows (GuassDePyramid.h:16) (blocking). */
 int gdp_download_level_rows(gdp_ctx* ctx, int b, int octave, int scale, float* const* rows);
+/* Copy rows [first_row, first_row + nrows) of level (o, s) of image b (rows as held by this
+ * context; a band context's row 0 is its first row) to a dense host array (blocking).  Reads one
+ * GaussPy[o][s][r] row range without materialising the level (e.g. 65536^2 images). */
+int gdp_download_level_range(gdp_ctx* ctx, int b, int octave, int scale, int first_row, int nrows, float* host);
 /* Copy the whole pyramid of image b in the packed layout [o][s][rows][cols] (blocking). */
 int gdp_download_pyramid(gdp_ctx* ctx, int b, float* host);
 /* Upload a packed pyramid of image b (state restore; used by re-entry tests). */

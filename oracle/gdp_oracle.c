@@ -111,6 +111,33 @@ void gdo_build(const int32_t* img, int H, int W, long pitch, int S, int O, float
     }
 }
 
+/*
+ * One row of every level of octave o — the closed form above restricted to level row r, for
+ * checking sampled rows of images too large to restate whole (65536^2: 114 GB of pyramid).
+ * in_row = input row r << o (W int32); out = [S+3][W >> o]; taps scratch >= 2*(S+3)*max(H,W).
+ */
+void gdo_level_row(const int32_t* in_row, int H, int W, int S, int o, int r, float* out, float* taps) {
+    const int L = S + 3, Wo = W >> o;
+    float* fc = taps;
+    float* fr = taps + (size_t)L * Wo;
+    float* hwin = fr + L; /* row-index taps: only entry r of each scale's H-axis window is used */
+    for (int s = 0; s < L; ++s) {
+        gdo_taps(W, o, s, fc + (size_t)s * Wo);
+        gdo_taps(H, o, s, hwin);
+        fr[s] = hwin[r];
+    }
+    for (int c = 0; c < Wo; ++c) {
+        const float x = (float)in_row[(size_t)c << o];
+        float g_prev = (x * fc[c]) * fr[0];
+        for (int s = 0; s + 1 < L; ++s) {
+            const float g_next = (x * fc[(size_t)(s + 1) * Wo + c]) * fr[s + 1];
+            out[(size_t)s * Wo + c] = g_prev - g_next;
+            g_prev = g_next;
+        }
+        out[(size_t)(L - 1) * Wo + c] = g_prev;
+    }
+}
+
 /* GaussPyInit refill (GuassDePyramid.h:74-86): every scale of octave o is (float)img[k<<o][l<<o]. */
 void gdo_init(const int32_t* img, int H, int W, long pitch, int S, int O, float* pyr) {
     for (int o = 0; o < O; ++o) {
@@ -230,6 +257,14 @@ static uint32_t gdo_mix32(uint32_t x) {
     x *= 0x846ca68bu;
     x ^= x >> 16;
     return x;
+}
+
+/* Row r of gdo_synthetic_image (W int32). */
+void gdo_synthetic_row(int32_t* row, int H, int W, uint32_t seed, long image_index, long r) {
+    for (long c = 0; c < W; ++c) {
+        const uint64_t idx = ((uint64_t)image_index * (uint64_t)H + (uint64_t)r) * (uint64_t)W + (uint64_t)c;
+        row[c] = (int32_t)(gdo_mix32(seed ^ (uint32_t)(idx ^ (idx >> 32))) >> 24);
+    }
 }
 
 void gdo_synthetic_image(int32_t* img, int H, int W, uint32_t seed, long image_index) {

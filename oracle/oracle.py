@@ -48,6 +48,8 @@ def lib():
         L.gdo_fnv.argtypes, L.gdo_fnv.restype = [p, sz], u64
         L.gdo_lcg_image.argtypes, L.gdo_lcg_image.restype = [p, i, i, u32], None
         L.gdo_synthetic_image.argtypes, L.gdo_synthetic_image.restype = [p, i, i, u32, lng], None
+        L.gdo_synthetic_row.argtypes, L.gdo_synthetic_row.restype = [p, i, i, u32, lng, lng], None
+        L.gdo_level_row.argtypes, L.gdo_level_row.restype = [p, i, i, i, i, i, p, p], None
         _lib = L
     return _lib
 
@@ -149,6 +151,22 @@ def synthetic_image(H, W, seed=0x5EED, index=0):
     img = np.empty((H, W), np.int32)
     lib().gdo_synthetic_image(_ptr(img), H, W, seed, index)
     return img
+
+
+def synthetic_row(H, W, r, seed=0x5EED, index=0):
+    """Row r of synthetic_image(H, W, seed, index)."""
+    row = np.empty(W, np.int32)
+    lib().gdo_synthetic_row(_ptr(row), H, W, seed, index, r)
+    return row
+
+
+def level_row(in_row, H, W, S, o, r):
+    """Row r of every level of octave o ([S+3][W >> o] float32) from input row r << o."""
+    in_row = np.ascontiguousarray(in_row, dtype=np.int32)
+    out = np.empty((S + 3, W >> o), np.float32)
+    scratch = np.empty(2 * (S + 3) * max(H, W) + 64, np.float32)
+    lib().gdo_level_row(_ptr(in_row), H, W, S, o, r, _ptr(out), _ptr(scratch))
+    return out
 
 
 def image_from_spec(n, spec):

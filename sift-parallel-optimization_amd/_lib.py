@@ -67,6 +67,7 @@ SIGNATURES = {
     "gdp_device_level": (_p, [_p, _c_int, _c_int, _c_int]),
     "gdp_download_level": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_download_level_rows": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_download_level_range": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _p]),
     "gdp_download_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_upload_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_packed_floats": (_c_size, [_p]),

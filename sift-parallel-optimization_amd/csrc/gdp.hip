@@ -44,6 +44,7 @@ constexpr int kFused = 5;       // octaves 0..4 share one 16 x 256 input tile
 constexpr int kTileRows = 16;   // 2^(kFused-1): every fused octave has whole rows in a tile
 constexpr int kTileCols = 256;  // tile width of the register octave-0 path (64 lanes x 4 pixels)
 constexpr int kLevelAlign = 64; // floats (256 B) — every level starts 16-B (and 256-B) aligned
+constexpr size_t kStageFloats = size_t(16) << 20;  // pinned D2H staging chunk (64 MiB)
 
 struct OctGeom {
     int rows;             // output rows of this octave held by the context (band-local)
@@ -1303,19 +1304,38 @@ int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) {
 int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows) {
     if (!valid_level(c, b, o, s) || !rows) return c ? c->status(GDP_ERR_ARG, "gdp_download_level_rows: bad argument") : GDP_ERR_ARG;
     const OctGeom& og = c->geom.oct[o];
-    const size_t nfl = (size_t)og.rows * og.cols;
-    if (nfl == 0) return GDP_OK;
+    if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
-    if (c->h_stage_floats < nfl) {  // one pinned buffer, grown to the largest level requested
+    // one pinned staging buffer of at most kStageFloats (or one row), reused chunk by chunk
+    const size_t chunk_rows = std::max<size_t>(1, std::min<size_t>(og.rows, kStageFloats / (size_t)og.cols));
+    const size_t nfl = chunk_rows * og.cols;
+    if (c->h_stage_floats < nfl) {
         if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
         c->h_stage = nullptr;
         c->h_stage_floats = 0;
         GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, nfl * 4, hipHostMallocDefault));
         c->h_stage_floats = nfl;
     }
-    GDP_HIP(c, hipMemcpyAsync(c->h_stage, gdp_device_level(c, b, o, s), nfl * 4, hipMemcpyDeviceToHost, c->stream));
+    const float* src = gdp_device_level(c, b, o, s);
+    for (size_t r0 = 0; r0 < (size_t)og.rows; r0 += chunk_rows) {
+        const size_t nr = std::min(chunk_rows, (size_t)og.rows - r0);
+        GDP_HIP(c, hipMemcpyAsync(c->h_stage, src + r0 * og.cols, nr * og.cols * 4, hipMemcpyDeviceToHost, c->stream));
+        GDP_HIP(c, hipStreamSynchronize(c->stream));
+        for (size_t r = 0; r < nr; ++r) std::memcpy(rows[r0 + r], c->h_stage + r * og.cols, (size_t)og.cols * 4);
+    }
+    return GDP_OK;
+}
+
+int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int nrows, float* host) {
+    if (!valid_level(c, b, o, s) || !host || first_row < 0 || nrows < 0 || first_row > c->geom.oct[o].rows ||
+        nrows > c->geom.oct[o].rows - first_row)
+        return c ? c->status(GDP_ERR_ARG, "gdp_download_level_range: bad argument") : GDP_ERR_ARG;
+    if (nrows == 0) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    const OctGeom& og = c->geom.oct[o];
+    GDP_HIP(c, hipMemcpyAsync(host, gdp_device_level(c, b, o, s) + (size_t)first_row * og.cols,
+                              (size_t)nrows * og.cols * 4, hipMemcpyDeviceToHost, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
-    for (int r = 0; r < og.rows; ++r) std::memcpy(rows[r], c->h_stage + (size_t)r * og.cols, (size_t)og.cols * 4);
     return GDP_OK;
 }
 

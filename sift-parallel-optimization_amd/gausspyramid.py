@@ -229,6 +229,15 @@ class PyramidContext:
             check(lib().gdp_download_level(self._ctx, int(b), int(o), int(s), _ptr(out)), self._ctx)
         return out
 
+    def level_range(self, b, o, s, first_row, nrows):
+        """Rows [first_row, first_row + nrows) of level (o, s) of image b, without downloading the
+        whole level."""
+        cols = self._dims[o][1]
+        out = np.empty((int(nrows), cols), np.float32)
+        check(lib().gdp_download_level_range(self._ctx, int(b), int(o), int(s), int(first_row), int(nrows),
+                                             _ptr(out)), self._ctx)
+        return out
+
     def level_rows(self, b, o, s, rows_out):
         """Download into a list of preallocated float32 row arrays (float**** materialisation)."""
         ptrs = (ctypes.c_void_p * len(rows_out))(*[r.ctypes.data for r in rows_out])

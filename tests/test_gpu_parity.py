@@ -383,6 +383,64 @@ def test_config5_16384_bands_equal_whole_image(pkg, oracle):
                 _assert_same(full.level(0, o, s)[r0:r1], want, ("c5 closed form", o, s))
 
 
+def test_row_downloads_chunked_and_ranged(pkg, oracle):
+    """float**** materialisation of a level larger than the 64-MiB pinned staging chunk (8192^2
+    level 0 = 4 chunks), and row-range downloads, == the dense level download."""
+    n = 8192
+    with pkg.PyramidContext(n, n, S=0, octaves=2) as ctx:
+        ctx.fill_synthetic(0x5EED, 1)
+        ctx.build()
+        for o in range(2):
+            dense = ctx.level(0, o, 2)
+            rows = [np.empty(n >> o, np.float32) for _ in range(n >> o)]
+            ctx.level_rows(0, o, 2, rows)
+            _assert_same(np.stack(rows), dense, ("rows", o))
+            for r0, nr in ((0, 1), (123, 77), ((n >> o) - 5, 5), (7, 0)):
+                _assert_same(ctx.level_range(0, o, 2, r0, nr), dense[r0:r0 + nr], ("range", o, r0, nr))
+        with pytest.raises(pkg.GdpError):
+            ctx.level_range(0, 0, 0, n - 1, 2)
+
+
+def test_max_size_65536_all_octaves(pkg, oracle):
+    """The largest square image one MI355X holds with its whole pyramid resident: 65536^2 = 2^32
+    input pixels (every pixel index past 32 bits), all 17 octaves (octaves >= 5 as tail units):
+    17.2 GB of int32 input + 114.5 GB of pyramid.  Sampled rows of every octave == the oracle's
+    row restatement (gdo_level_row, pinned to the closed form); the device checksum of the fused
+    build == that of the reference-order in-place path (GaussPyInit refill + GenerateDoG,
+    k_levels); at 5 octaves the whole image's checksum == the sum of its two row bands'."""
+    n, S = 65536, 2
+    rng = np.random.default_rng(65536)
+    with pkg.PyramidContext(n, n, S=S, octaves=0) as ctx:
+        O = ctx.O
+        assert O == 17
+        ctx.fill_synthetic(0x5EED, 0)
+        ctx.build()
+        ctx.sync()
+        for o in range(O):
+            Ho = n >> o
+            rows = {0, Ho // 2, Ho - 1} | {int(r) for r in rng.integers(0, Ho, 2)}
+            for r in sorted(rows):
+                want = oracle.level_row(oracle.synthetic_row(n, n, r << o, 0x5EED, 0), n, n, S, o, r)
+                for s in range(S + 3):
+                    _assert_same(ctx.level_range(0, o, s, r, 1)[0], want[s], ("65536", o, s, r))
+        built = ctx.checksum(0)
+        ctx.init()
+        ctx.generate_dog()
+        assert ctx.checksum(0) == built
+    # row bands must be multiples of 2^(O-1) rows, so the band split runs at O = 5 (config 5's)
+    with pkg.PyramidContext(n, n, S=S, octaves=5) as ctx:
+        ctx.fill_synthetic(0x5EED, 0)
+        ctx.build()
+        whole5 = ctx.checksum(0)
+    total = 0
+    for r0, r1 in ((0, n // 2), (n // 2, n)):
+        with pkg.PyramidContext(n, n, S=S, octaves=5, row_begin=r0, row_end=r1) as band:
+            band.fill_synthetic(0x5EED, 0)
+            band.build()
+            total = (total + band.checksum(0)) & 0xFFFFFFFFFFFFFFFF
+    assert total == whole5
+
+
 # ------------------------------------------------------------------ checksum / zero-copy output / mgpu
 def test_device_checksum_matches_reference(pkg, oracle, golden):
     """gdp_checksum of the GPU pyramid == the checksum of the reference's own output, incl. the

@@ -28,10 +28,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss"])
     ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
+    ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
     args = ap.parse_args()
     pkg = entry.load_package()
     cfg = bench.CONFIGS[args.config]
     H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
+    if args.shape:
+        H, W, B = (int(x) for x in args.shape.split("x"))
     ctx = pkg.PyramidContext(H, W, S=2, octaves=O, batch=B)
     ctx.fill_synthetic(bench.SEED, 0)
     ctx.sync()
@@ -86,7 +89,7 @@ def main():
         nbytes = 8 * 5 * B * sum((H >> o) * (W >> o) for o in range(O))
     for name, _ in variants:
         t = np.array(times[name])
-        print(json.dumps({"variant": name, "config": args.config, "ms_median": round(float(np.median(t)), 5),
+        print(json.dumps({"variant": name, "config": args.config, "shape": [H, W, B], "ms_median": round(float(np.median(t)), 5),
                           "ms_min": round(float(t.min()), 5),
                           "GBps_median": round(nbytes / (np.median(t) / 1e3) / 1e9, 1)}), flush=True)
     ctx.close()
