@@ -188,6 +188,8 @@ def main():
                     help="build: fused GaussPyInit+GenerateDoG (headline); regen: in-place GenerateDoG "
                          "re-entry; gauss: in-place row+column window pass of every octave; conv: the "
                          "true-Gaussian-convolution extension (not the reference's algorithm)")
+    ap.add_argument("--conv-kernel", type=int, default=None, help="--op conv: 0 register sweep, 1 LDS tiles")
+    ap.add_argument("--conv-rows", type=int, default=None, help="--op conv sweep: rows per wave strip (16/32/64)")
     args = ap.parse_args()
 
     import torch
@@ -238,6 +240,7 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
+    ctx.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows)
     autotuned = None
     if args.variant is not None:
         ctx.set_tuning(variant=args.variant)
@@ -314,7 +317,10 @@ def main():
                        if args.op == "build" else
                        {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
                         "gauss": "k_window (in-place row+column window, all octaves)",
-                        "conv": "k_conv (extension: separable Gaussian convolution, LDS halo tiles)"}[args.op]),
+                        "conv": ("k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
+                                 "DPP lane shifts, %d-row strips)" % ctx.tuning()["conv_rows"]
+                                 if ctx.tuning()["conv_kernel"] == 0 and S <= 3 else
+                                 "k_conv (extension: separable Gaussian convolution, LDS halo tiles)")}[args.op]),
             "kernel_ms": round(kernel_ms, 6),
             "algorithmic_bytes_per_launch": bytes_launch,
         },

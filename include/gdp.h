@@ -191,7 +191,9 @@ enum {
                                    2 XCD row-interleaved                                       */
     GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk
                                    (1 default, 2 or 4)                                         */
-    GDP_TUNE_WINDOW_SUB = 7     /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
+    GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
+    GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (default, S <= 3), 1 LDS tiles */
+    GDP_TUNE_CONV_ROWS = 9      /* gdp_build_gaussian sweep: output rows per wave strip (16 default, 32, 64) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

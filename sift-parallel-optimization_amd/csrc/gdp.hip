@@ -25,6 +25,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "gdp.h"
@@ -92,6 +94,10 @@ struct Geom {
     unsigned lv_blk[kMaxOct + 1]; // prefix over octaves of ceil(rows*gpr / kLevBlock) per image
     unsigned cv_blk[kMaxOct + 1]; // convolution mode: prefix over octaves of 16x256 output tiles
     int cv_tiles_c[kMaxOct];      // convolution mode: tile columns per octave
+    unsigned sw_blk[kMaxOct + 1]; // convolution sweep: prefix over octaves of blocks (4 strips of T rows);
+                                  // octaves whose width is not a multiple of 4 count 0 (tiles do them)
+    int sw_strips_c[kMaxOct];     // convolution sweep: 240-column strips per octave
+    unsigned cvx_blk[kMaxOct + 1]; // convolution tiles for the octaves the sweep skips
 };
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -580,16 +586,17 @@ __device__ __forceinline__ void conv_pass(const float* __restrict__ in_s, float*
 template <bool NT>
 __global__ void __launch_bounds__(256, 3) k_conv(const Geom* __restrict__ g, const void* __restrict__ in,
                                                  float* __restrict__ out, const float* __restrict__ ctaps,
-                                                 const int* __restrict__ cradius) {
+                                                 const int* __restrict__ cradius, int rest) {
     __shared__ __attribute__((aligned(16))) float in_s[kCvInH * kCvInW];
     __shared__ __attribute__((aligned(16))) float h_s[kCvTH * kCvInW];
-    const unsigned per = g->cv_blk[g->O];
+    const unsigned* pre = rest ? g->cvx_blk : g->cv_blk; // rest: only the octaves the sweep skips
+    const unsigned per = pre[g->O];
     const unsigned b = blockIdx.x / per;
     const unsigned v = blockIdx.x - b * per;
     int o = 0;
-    while (o + 1 < g->O && v >= g->cv_blk[o + 1]) ++o;
+    while (o + 1 < g->O && v >= pre[o + 1]) ++o;
     const OctGeom og = g->oct[o];
-    const unsigned t = v - g->cv_blk[o];
+    const unsigned t = v - pre[o];
     const int tr = (int)(t / (unsigned)g->cv_tiles_c[o]);
     const int tc = (int)(t - (unsigned)tr * (unsigned)g->cv_tiles_c[o]);
     const int r0 = tr * kCvTH, c0 = tc * kCvTW; // octave-o output coordinates of the tile
@@ -659,6 +666,239 @@ __global__ void __launch_bounds__(256, 3) k_conv(const Geom* __restrict__ g, con
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) store(g->L - 1, q, prev[q]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Convolution extension, register-sweep form (default; k_conv above is the LDS-tile form kept for
+// A/B).  One wave owns a strip of 240 output columns x T output rows of one octave; each lane holds
+// 4 consecutive columns (lanes 0-1 and 62-63 carry the 8-column left / right halo and store
+// nothing).  No LDS and no barriers:
+//  * vertical pass in registers: the wave walks down its T + 2*6 input rows once (int4 loads of
+//    the decimated base, clamp-to-edge), and every scale's vertical sum reuses the same symmetric
+//    pair sums x[i+d] + x[i-d] (taps are symmetric), so all S+3 scales cost sum(R_s + 1) FMAs;
+//  * horizontal pass across lanes: the neighbouring columns come from lanes l +- 1, l +- 2 through
+//    DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1, fused into the FMAs by the compiler);
+//  * DoG against the previous scale in registers, 960-B contiguous wave stores per level row.
+// Four waves per block take four vertically adjacent strips, so their shared halo rows are read
+// from L2 at the same time.  Radii are compile-time (R_s = ceil(3 sigma_s), sigma_s = 2/(s+1)); the
+// tap values come from gdp_conv_taps.
+// ------------------------------------------------------------------------------------------
+constexpr int kSwLanesOut = 60;                // lanes 2..61 produce output
+constexpr int kSwCols = 4 * kSwLanesOut;       // output columns per wave strip
+constexpr int kSwHalo = 8;                     // input columns left of the strip's first column
+constexpr int kSwWaves = 4;                    // vertically adjacent strips per block
+
+__host__ __device__ constexpr int conv_radius_of(int s) {
+    return (6 + s) / (s + 1) > kCvR ? kCvR : ((6 + s) / (s + 1) < 1 ? 1 : (6 + s) / (s + 1));
+}
+
+// Normalised Gaussian taps of scale s as compile-time constants (the kernel's FMA operands) and
+// for gdp_conv_taps on the host — one definition, so host and device agree bit for bit.
+// e^x for 0 <= x <= 13 by its (positive, non-cancelling) Taylor series in double.
+__host__ __device__ constexpr double conv_exp_pos(double x) {
+    double term = 1.0, sum = 1.0;
+    for (int n = 1; n < 100; ++n) {
+        term *= x / n;
+        sum += term;
+    }
+    return sum;
+}
+__host__ __device__ constexpr double conv_weight(int s, int d) { // exp(-d^2 / (2 sigma_s^2))
+    return 1.0 / conv_exp_pos((double)d * d * (s + 1) * (s + 1) / 8.0); // sigma_s = 2 / (s + 1)
+}
+struct ConvTaps {
+    float k[kCvR + 1]; // k[|d|], d = -R..R
+};
+__host__ __device__ constexpr ConvTaps conv_taps_of(int s) {
+    const int R = conv_radius_of(s);
+    double sum = 0.0;
+    for (int d = -R; d <= R; ++d) sum += conv_weight(s, d);
+    ConvTaps t{};
+    for (int d = 0; d <= R; ++d) t.k[d] = (float)(conv_weight(s, d) / sum);
+    return t;
+}
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// lane l receives lane l-1's (prev) / lane l+1's (next) value; the wave's end lanes receive 0
+__device__ __forceinline__ float lane_prev(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_next(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+// Horizontal symmetric filter of radius R over the wave-distributed row v (4 columns per lane):
+// out_j = k[0] a_j + sum_{d=1..R} k[d] (a_{j+d} + a_{j-d}), a_m = column 4l + m.
+template <int s>
+__device__ __forceinline__ f4 conv_h_lanes(f4 v) {
+    constexpr int R = conv_radius_of(s);
+    constexpr ConvTaps K = conv_taps_of(s);
+    static_assert(R >= 1 && R <= 8, "radius");
+    const float c[4] = {v.x, v.y, v.z, v.w};
+    float p1[4] = {0.f, 0.f, 0.f, 0.f}, n1[4] = {0.f, 0.f, 0.f, 0.f};
+    float p2[4] = {0.f, 0.f, 0.f, 0.f}, n2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j >= 4 - R) p1[j] = lane_prev(c[j]); // column 4l - 4 + j
+        if (j <= R - 1) n1[j] = lane_next(c[j]); // column 4l + 4 + j
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (R > 4 && j >= 8 - R) p2[j] = lane_prev(p1[j]); // column 4l - 8 + j
+        if (R > 4 && j <= R - 5) n2[j] = lane_next(n1[j]); // column 4l + 8 + j
+    }
+    auto a = [&](int m) -> float {
+        return m < -4 ? p2[m + 8] : m < 0 ? p1[m + 4] : m < 4 ? c[m] : m < 8 ? n1[m - 4] : n2[m - 8];
+    };
+    float out[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float acc = K.k[0] * a(j);
+#pragma unroll
+        for (int d = 1; d <= R; ++d) acc = __builtin_fmaf(K.k[d], a(j + d) + a(j - d), acc);
+        out[j] = acc;
+    }
+    return f4{out[0], out[1], out[2], out[3]};
+}
+
+// Buffer resources for the sweep: with raw buffer loads/stores every memory instruction is issued
+// unconditionally (disabled lanes get an offset past num_records: the store is dropped), so the
+// compiler can count outstanding loads exactly (s_waitcnt vmcnt(N), not vmcnt(0) after every
+// skip-branch around a store), and all row addressing is scalar (SGPR base per row / level).
+constexpr int kOOB = 0x7FFFFFF0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, kOOB, 0x00020000);
+}
+enum { kLdVecI32 = 0, kLdVecU8 = 1, kLdScalarI32 = 2, kLdScalarU8 = 3 };
+
+template <int L, int T, bool NT, int LD>
+__device__ __forceinline__ void conv_sweep_body(const Geom* __restrict__ g, const OctGeom& og, const void* __restrict__ in,
+                                                float* __restrict__ out, int b, int o, int R0, int cin, int lane) {
+    constexpr int kWin = 2 * kCvR + 1; // input rows one output row needs
+    constexpr int kRing = kWin + 3;    // + 3 rows of prefetch: a 16-row register ring
+    static_assert(T % kRing == 0, "strip rows must be a multiple of the ring");
+    constexpr int esz = (LD == kLdVecU8 || LD == kLdScalarU8) ? 1 : 4;
+    const int rows = og.rows, cols = og.cols;
+    // per-lane column offsets (bytes within an input row).  Vector loads: cin and cols are
+    // multiples of 4, so a halo group is either inside the row, wholly left of it (every column
+    // clamps to column 0: broadcast .x of the group at 0) or wholly right of it (broadcast .w of
+    // the last group)
+    int voff[4];
+    const int cl = min(max(cin, 0), max(cols - 4, 0));
+    const bool left = cin < 0, right = cin >= cols;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        voff[j] = (LD == kLdVecI32 || LD == kLdVecU8) ? cl * esz : (min(max(cin + j, 0), cols - 1) << o) * esz;
+    auto clamp_group = [&](f4 w) -> f4 {
+        const float lo = right ? w.w : w.x, hi = left ? w.x : w.w;
+        return f4{lo, left ? w.x : (right ? w.w : w.y), left ? w.x : (right ? w.w : w.z), hi};
+    };
+    const char* img = static_cast<const char*>(in) + (long long)b * g->in_img_stride * esz;
+    const long long row_bytes = ((long long)g->in_pitch << o) * esz; // input bytes between octave-o rows
+    auto load = [&](int q) -> f4 {                                    // input row R0 - kCvR + q (clamped)
+        const int r = min(max(R0 - kCvR + q, 0), rows - 1);           // wave-uniform
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(img + (long long)r * row_bytes);
+        if constexpr (LD == kLdVecI32) {
+            const i4 w = __builtin_bit_cast(i4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[0], 0, 0));
+            return clamp_group(__builtin_convertvector(w, f4));
+        } else if constexpr (LD == kLdVecU8) {
+            const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(rs, voff[0], 0, 0);
+            return clamp_group(f4{(float)(w & 0xffu), (float)((w >> 8) & 0xffu), (float)((w >> 16) & 0xffu),
+                                  (float)(w >> 24)});
+        } else {
+            float x[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (LD == kLdScalarI32)
+                    x[j] = (float)(int)__builtin_amdgcn_raw_buffer_load_b32(rs, voff[j], 0, 0);
+                else
+                    x[j] = (float)__builtin_amdgcn_raw_buffer_load_b8(rs, voff[j], 0, 0);
+            }
+            return f4{x[0], x[1], x[2], x[3]};
+        }
+    };
+    // one store resource per level, based at this wave's first row; lanes 0-1 / 62-63 (halo) and
+    // columns past the row end store out of range
+    const bool active = lane >= 2 && lane < 2 + kSwLanesOut && cin < cols;
+    const int soff_lane = active ? cin * 4 : kOOB;
+    float* lev0 = out + (long long)b * g->pyr_stride + og.lev_off + (long long)R0 * cols;
+    __amdgpu_buffer_rsrc_t rs_out[L];
+#pragma unroll
+    for (int s = 0; s < L; ++s) rs_out[s] = make_rsrc(lev0 + (long long)s * og.lev_stride);
+    // soffset stays the constant 0: with an SGPR soffset the compiler omits the wait state that a
+    // VALU overwrite of a >8-byte store's data VGPRs needs right after the store, and gfx950 then
+    // stores the overwritten values (measured); the row offset goes into voffset instead
+    auto store_b128 = [&](f4 val, __amdgpu_buffer_rsrc_t rs, int vo) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, val), rs, vo, 0, NT ? 2 : 0);
+    };
+    // ring of input rows: slot q % kRing holds input row R0 - kCvR + q
+    f4 x[kRing];
+#pragma unroll
+    for (int q = 0; q < kRing; ++q) x[q] = load(q);
+#pragma unroll 1
+    for (int i0 = 0; i0 < T && R0 + i0 < rows; i0 += kRing) {
+#pragma unroll
+        for (int u = 0; u < kRing; ++u) {
+            const int i = i0 + u; // output row R0 + i needs ring slots (u + 0..12) % kRing
+            f4 pr[kCvR + 1];      // symmetric pair sums, shared by every scale
+            pr[0] = x[(u + kCvR) % kRing];
+#pragma unroll
+            for (int d = 1; d <= kCvR; ++d) pr[d] = x[(u + kCvR + d) % kRing] + x[(u + kCvR - d) % kRing];
+            if (i + kRing < T + 2 * kCvR) x[u] = load(i + kRing); // refill the slot just used (uniform)
+            const int vo = (R0 + i < rows ? soff_lane : kOOB) + i * cols * 4; // OOB stays OOB (< 2^32)
+            f4 hprev = {0.f, 0.f, 0.f, 0.f};
+            static_for<L>([&](auto si) {
+                constexpr int s = decltype(si)::value;
+                constexpr int R = conv_radius_of(s);
+                constexpr ConvTaps K = conv_taps_of(s);
+                f4 vs = pr[0] * K.k[0];
+#pragma unroll
+                for (int d = 1; d <= R; ++d) vs = fma4(K.k[d], pr[d], vs);
+                const f4 h = conv_h_lanes<s>(vs);
+                if constexpr (s > 0) store_b128(hprev - h, rs_out[s - 1], vo);
+                hprev = h;
+            });
+            store_b128(hprev, rs_out[L - 1], vo);
+        }
+    }
+}
+
+template <int L, int T, bool NT>
+__global__ void __launch_bounds__(64 * kSwWaves, 4) k_conv_sweep(const Geom* __restrict__ g, const void* __restrict__ in,
+                                                                 float* __restrict__ out) {
+    const unsigned per = g->sw_blk[g->O];
+    const unsigned b = blockIdx.x / per;
+    const unsigned v = blockIdx.x - b * per;
+    int o = 0;
+    while (o + 1 < g->O && v >= g->sw_blk[o + 1]) ++o;
+    const OctGeom og = g->oct[o];
+    const unsigned t = v - g->sw_blk[o];
+    const unsigned sc = (unsigned)g->sw_strips_c[o];
+    const int tr = (int)(t / sc), tc = (int)(t - (unsigned)tr * sc);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int R0 = (tr * kSwWaves + wave) * T; // first output row of this wave
+    if (R0 >= og.rows) return;                 // whole waves only; no barriers in this kernel
+    const int cin = tc * kSwCols - kSwHalo + 4 * lane;
+    if (o == 0 && g->vec_in && og.cols >= 4) {
+        if (g->in_fmt == GDP_INPUT_U8)
+            conv_sweep_body<L, T, NT, kLdVecU8>(g, og, in, out, (int)b, o, R0, cin, lane);
+        else
+            conv_sweep_body<L, T, NT, kLdVecI32>(g, og, in, out, (int)b, o, R0, cin, lane);
+    } else if (g->in_fmt == GDP_INPUT_U8) {
+        conv_sweep_body<L, T, NT, kLdScalarU8>(g, og, in, out, (int)b, o, R0, cin, lane);
+    } else {
+        conv_sweep_body<L, T, NT, kLdScalarI32>(g, og, in, out, (int)b, o, R0, cin, lane);
+    }
 }
 
 // Order-independent pyramid checksum (verification of multi-GPU runs without moving pyramids):
@@ -776,6 +1016,8 @@ struct gdp_ctx {
     const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
     float* d_taps = nullptr;
+    int conv_kernel = 0;          // GDP_TUNE_CONV_KERNEL: 0 register sweep (default), 1 LDS tiles
+    int conv_rows = 16;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
     int* d_cradius = nullptr;     // convolution-mode radius per scale
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
@@ -910,6 +1152,37 @@ bool valid_level(const gdp_ctx* c, int b, int o, int s) {
 // ==========================================================================================
 // C ABI
 // ==========================================================================================
+// Block prefix of the convolution sweep (kSwWaves strips of conv_rows rows x kSwCols columns).
+static void conv_sweep_geom(gdp_ctx* c) {
+    Geom& g = c->geom;
+    g.sw_blk[0] = 0;
+    g.cvx_blk[0] = 0;
+    for (int o = 0; o < g.O; ++o) {
+        const OctGeom& og = g.oct[o];
+        const bool sweep = og.cols >= 4 && og.cols % 4 == 0; // full 16-B stores on every row
+        g.sw_strips_c[o] = (og.cols + kSwCols - 1) / kSwCols;
+        const long long rows_per_blk = (long long)kSwWaves * c->conv_rows;
+        g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
+        g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
+    }
+}
+
+template <int L, int T>
+hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned grid, hipStream_t st) {
+    auto k = c->nontemporal ? k_conv_sweep<L, T, true> : k_conv_sweep<L, T, false>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kSwWaves), 0, st, c->d_geom, c->d_in, c->d_out);
+    return hipGetLastError();
+}
+
+template <int L>
+hipError_t launch_conv_sweep_l(gdp_ctx* c, unsigned grid, hipStream_t st) {
+    switch (c->conv_rows) {
+        case 32: return launch_conv_sweep_t<L, 32>(c, grid, st);
+        case 64: return launch_conv_sweep_t<L, 64>(c, grid, st);
+        default: return launch_conv_sweep_t<L, 16>(c, grid, st);
+    }
+}
+
 extern "C" {
 
 int gdp_abi_version(void) { return GDP_ABI_VERSION; }
@@ -1029,6 +1302,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // tiles; batches and <= 4096^2 images are fastest in linear order.
     g.tile_order = (batch == 1 && (long long)g.in_rows * W >= (1ll << 26)) ? 1 : 0;
     retile(c, kVariants[c->variant].tile_cols, kVariants[c->variant].tile_rows);
+    conv_sweep_geom(c);
     c->h_taps.assign((size_t)tap_off, 0.0f);
     for (int o = 0; o < O; ++o) {
         const OctGeom& og = g.oct[o];
@@ -1222,11 +1496,9 @@ int gdp_build(gdp_ctx* c, void* stream) {
 
 int gdp_conv_taps(int S, int scale, float* taps, int* radius) {
     if (S < 0 || scale < 0 || scale >= S + 3 || !taps || !radius) return GDP_ERR_ARG;
-    const double sig = (double)kSigma / (scale + 1);
-    const int R = std::min(kCvR, std::max(1, (int)std::ceil(3.0 * sig)));
-    double w[kCvMaxTaps], sum = 0;
-    for (int d = -R; d <= R; ++d) sum += (w[d + R] = std::exp(-(double)d * d / (2.0 * sig * sig)));
-    for (int j = 0; j < kCvMaxTaps; ++j) taps[j] = j <= 2 * R ? (float)(w[j] / sum) : 0.0f;
+    const int R = conv_radius_of(scale); // ceil(3 sigma), sigma = 2 / (scale + 1), at most kCvR
+    const ConvTaps k = conv_taps_of(scale);
+    for (int j = 0; j < kCvMaxTaps; ++j) taps[j] = j <= 2 * R ? k.k[j < R ? R - j : j - R] : 0.0f;
     *radius = R;
     return GDP_OK;
 }
@@ -1246,11 +1518,27 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) {
         GDP_HIP(c, hipMemcpy(c->d_ctaps, t.data(), t.size() * 4, hipMemcpyHostToDevice));
         GDP_HIP(c, hipMemcpy(c->d_cradius, r.data(), r.size() * 4, hipMemcpyHostToDevice));
     }
-    const long long grid = (long long)g.cv_blk[g.O] * g.batch;
+    const hipStream_t st = c->pick(stream);
+    // the register sweep is compiled for S = 0..3 (L = 3..6) and takes the octaves whose width is a
+    // multiple of 4; the LDS tiles take the rest (and everything for other S or conv_kernel = 1)
+    const bool sweep = c->conv_kernel == 0 && g.L >= 3 && g.L <= 6;
+    if (sweep) {
+        const long long grid = (long long)g.sw_blk[g.O] * g.batch;
+        if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
+        if (grid > 0) {
+            switch (g.L) {
+                case 3: GDP_HIP(c, launch_conv_sweep_l<3>(c, (unsigned)grid, st)); break;
+                case 4: GDP_HIP(c, launch_conv_sweep_l<4>(c, (unsigned)grid, st)); break;
+                case 5: GDP_HIP(c, launch_conv_sweep_l<5>(c, (unsigned)grid, st)); break;
+                default: GDP_HIP(c, launch_conv_sweep_l<6>(c, (unsigned)grid, st)); break;
+            }
+        }
+    }
+    const long long grid = (long long)(sweep ? g.cvx_blk[g.O] : g.cv_blk[g.O]) * g.batch;
     if (grid <= 0) return GDP_OK;
     if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
-    hipLaunchKernelGGL(c->nontemporal ? k_conv<true> : k_conv<false>, dim3((unsigned)grid), dim3(256), 0, c->pick(stream),
-                       c->d_geom, c->d_in, c->d_out, c->d_ctaps, c->d_cradius);
+    hipLaunchKernelGGL(c->nontemporal ? k_conv<true> : k_conv<false>, dim3((unsigned)grid), dim3(256), 0, st,
+                       c->d_geom, c->d_in, c->d_out, c->d_ctaps, c->d_cradius, sweep ? 1 : 0);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
 }
@@ -1471,6 +1759,8 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_TILE_ORDER: *value = c->geom.tile_order; return GDP_OK;
         case GDP_TUNE_INPLACE_SUB: *value = c->inplace_sub; return GDP_OK;
         case GDP_TUNE_WINDOW_SUB: *value = c->window_sub; return GDP_OK;
+        case GDP_TUNE_CONV_KERNEL: *value = c->conv_kernel; return GDP_OK;
+        case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 }
@@ -1495,6 +1785,22 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             if (value != 1 && value != 2 && value != 4) return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4");
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
+        case GDP_TUNE_CONV_KERNEL:
+            if (value != 0 && value != 1) return c->status(GDP_ERR_ARG, "conv kernel must be 0 (sweep) or 1 (tiles)");
+            c->conv_kernel = value;
+            return GDP_OK;
+        case GDP_TUNE_CONV_ROWS: {
+            if (value != 16 && value != 32 && value != 64) return c->status(GDP_ERR_ARG, "conv rows must be 16, 32 or 64");
+            const int old = c->conv_rows;
+            c->conv_rows = value;
+            conv_sweep_geom(c);
+            const int rc = upload_geom(c);
+            if (rc != GDP_OK) {
+                c->conv_rows = old;
+                conv_sweep_geom(c);
+            }
+            return rc;
+        }
         case GDP_TUNE_TILE_ORDER:
             if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");
             c->geom.tile_order = value;

@@ -181,17 +181,26 @@ class PyramidContext:
     def stream(self):
         return lib().gdp_stream(self._ctx)
 
-    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None,
-                   inplace_sub=None, window_sub=None):
-        """Performance knobs of the kernels (outputs are bit-identical for every setting)."""
-        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_INPLACE_SUB, GDP_TUNE_NONTEMPORAL,
-                           GDP_TUNE_TILE_ORDER, GDP_TUNE_VARIANT, GDP_TUNE_WINDOW_SUB)
+    _TUNING = ("nontemporal", "blocks_per_cu", "grid", "variant", "tile_order", "inplace_sub", "window_sub",
+               "conv_kernel", "conv_rows")
 
-        for key, val in ((GDP_TUNE_NONTEMPORAL, nontemporal), (GDP_TUNE_BLOCKS_PER_CU, blocks_per_cu),
-                         (GDP_TUNE_GRID, grid), (GDP_TUNE_VARIANT, variant), (GDP_TUNE_TILE_ORDER, tile_order),
-                         (GDP_TUNE_INPLACE_SUB, inplace_sub), (GDP_TUNE_WINDOW_SUB, window_sub)):
-            if val is not None:
-                check(lib().gdp_set_tuning(self._ctx, key, int(val)), self._ctx)
+    @staticmethod
+    def _tuning_key(name):
+        from . import _lib
+
+        return getattr(_lib, "GDP_TUNE_" + name.upper())
+
+    def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None,
+                   inplace_sub=None, window_sub=None, conv_kernel=None, conv_rows=None):
+        """Performance knobs of the kernels (outputs are bit-identical for every setting; the
+        conv_* knobs select the convolution extension's kernel: 0 register sweep, 1 LDS tiles, and
+        the sweep's rows per wave strip)."""
+        vals = dict(nontemporal=nontemporal, blocks_per_cu=blocks_per_cu, grid=grid, variant=variant,
+                    tile_order=tile_order, inplace_sub=inplace_sub, window_sub=window_sub, conv_kernel=conv_kernel,
+                    conv_rows=conv_rows)
+        for name in self._TUNING:
+            if vals[name] is not None:
+                check(lib().gdp_set_tuning(self._ctx, self._tuning_key(name), int(vals[name])), self._ctx)
 
     def autotune(self, iters=5, stream=None):
         """Time every build variant x tile order on the current input and keep the fastest;
@@ -202,16 +211,11 @@ class PyramidContext:
         return v.value, o.value, ms.value
 
     def tuning(self):
-        """Current {nontemporal, blocks_per_cu, grid, variant} of the build kernel."""
-        from ._lib import (GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_INPLACE_SUB, GDP_TUNE_NONTEMPORAL,
-                           GDP_TUNE_TILE_ORDER, GDP_TUNE_VARIANT, GDP_TUNE_WINDOW_SUB)
-
+        """Current value of every knob of set_tuning()."""
         out = {}
-        for name, key in (("nontemporal", GDP_TUNE_NONTEMPORAL), ("blocks_per_cu", GDP_TUNE_BLOCKS_PER_CU),
-                          ("grid", GDP_TUNE_GRID), ("variant", GDP_TUNE_VARIANT), ("tile_order", GDP_TUNE_TILE_ORDER),
-                          ("inplace_sub", GDP_TUNE_INPLACE_SUB), ("window_sub", GDP_TUNE_WINDOW_SUB)):
+        for name in self._TUNING:
             v = _i()
-            check(lib().gdp_get_tuning(self._ctx, key, ctypes.byref(v)), self._ctx)
+            check(lib().gdp_get_tuning(self._ctx, self._tuning_key(name), ctypes.byref(v)), self._ctx)
             out[name] = v.value
         return out
 

@@ -574,22 +574,33 @@ def _conv_reference(pkg, img, S, O):
     return out
 
 
-@pytest.mark.parametrize("H,W,S,O,fmt", [(64, 96, 2, 0, "i32"), (300, 500, 3, 5, "i32"), (1080, 1920, 2, 5, "u8"),
-                                          (17, 33, 1, 0, "i32")])
-def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt):
+_CONV_SHAPES = [(64, 96, 2, 0, "i32", 1), (300, 500, 3, 5, "i32", 1), (1080, 1920, 2, 5, "u8", 1),
+                (17, 33, 1, 0, "i32", 1), (70, 240, 0, 0, "i32", 2), (129, 484, 2, 4, "i32", 1), (40, 50, 5, 0, "i32", 1)]
+_CONV_KERNELS = [dict(conv_kernel=0, conv_rows=32), dict(conv_kernel=0, conv_rows=16), dict(conv_kernel=0, conv_rows=64),
+                 dict(conv_kernel=1)]
+
+
+@pytest.mark.parametrize("H,W,S,O,fmt,batch", _CONV_SHAPES)
+@pytest.mark.parametrize("tune", _CONV_KERNELS, ids=["sweep32", "sweep16", "sweep64", "tiles"])
+def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt, batch, tune):
     """Extension mode (no reference counterpart; parity unpinned by construction): checked against
-    a float64 separable convolution.  Tolerance: |gpu - ref| <= 1e-3 + 1e-5 |ref| (float32
-    accumulation of <= 13 taps on pixels <= 255)."""
-    img = oracle.lcg_image(H, W, 21)
+    a float64 separable convolution, for both kernels (register sweep with DPP lane shifts, LDS
+    tiles) — strip edges at 240/480 columns, rows fewer than a strip, batches, S = 5 (falls back
+    to the tiles).  Tolerance: |gpu - ref| <= 1e-3 + 1e-5 |ref| (float32 accumulation of <= 13
+    taps on pixels <= 255)."""
+    imgs = [oracle.lcg_image(H, W, 21 + b) for b in range(batch)]
     if fmt == "u8":
-        img = img.astype(np.uint8)
-    with pkg.PyramidContext(H, W, S=S, octaves=O, input_format=fmt) as ctx:
-        ctx.set_input(img)
+        imgs = [im.astype(np.uint8) for im in imgs]
+    with pkg.PyramidContext(H, W, S=S, octaves=O, batch=batch, input_format=fmt) as ctx:
+        ctx.set_tuning(**tune)
+        for b, im in enumerate(imgs):
+            ctx.set_input(im, b)
         ctx.build_gaussian()
         ctx.sync()
-        want = _conv_reference(pkg, img.astype(np.int32), S, ctx.O)
-        for (o, s), ref in want.items():
-            got = ctx.level(0, o, s).astype(np.float64)
-            assert got.shape == ref.shape
-            err = np.abs(got - ref) - (1e-3 + 1e-5 * np.abs(ref))
-            assert err.max() <= 0, ((o, s), float(np.abs(got - ref).max()))
+        for b, im in enumerate(imgs):
+            want = _conv_reference(pkg, im.astype(np.int32), S, ctx.O)
+            for (o, s), ref in want.items():
+                got = ctx.level(b, o, s).astype(np.float64)
+                assert got.shape == ref.shape
+                err = np.abs(got - ref) - (1e-3 + 1e-5 * np.abs(ref))
+                assert err.max() <= 0, ((b, o, s), float(np.abs(got - ref).max()))
