@@ -189,7 +189,8 @@ def main():
                          "re-entry; gauss: in-place row+column window pass of every octave; conv: the "
                          "true-Gaussian-convolution extension (not the reference's algorithm)")
     ap.add_argument("--conv-kernel", type=int, default=None, help="--op conv: 0 register sweep, 1 LDS tiles")
-    ap.add_argument("--conv-rows", type=int, default=None, help="--op conv sweep: rows per wave strip (16/32/64)")
+    ap.add_argument("--conv-rows", type=int, default=None, help="--op conv sweep: rows per wave strip (16/32)")
+    ap.add_argument("--conv-order", type=int, default=None, help="--op conv sweep: bit 0 XCD-chunked, bit 1 alternate directions")
     args = ap.parse_args()
 
     import torch
@@ -240,7 +241,7 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
-    ctx.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows)
+    ctx.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order)
     autotuned = None
     if args.variant is not None:
         ctx.set_tuning(variant=args.variant)

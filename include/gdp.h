@@ -193,7 +193,9 @@ enum {
                                    (1 default, 2 or 4)                                         */
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (default, S <= 3), 1 LDS tiles */
-    GDP_TUNE_CONV_ROWS = 9      /* gdp_build_gaussian sweep: output rows per wave strip (16 default, 32, 64) */
+    GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian sweep: output rows per wave strip (16 default, 32) */
+    GDP_TUNE_CONV_ORDER = 11    /* gdp_build_gaussian sweep: bit 0 XCD-chunked block order, bit 1 odd waves
+                                   sweep bottom-up (shared halo rows loaded together); default 0 */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

@@ -670,23 +670,45 @@ __global__ void __launch_bounds__(256, 3) k_conv(const Geom* __restrict__ g, con
 
 // ------------------------------------------------------------------------------------------
 // Convolution extension, register-sweep form (default; k_conv above is the LDS-tile form kept for
-// A/B).  One wave owns a strip of 240 output columns x T output rows of one octave; each lane holds
-// 4 consecutive columns (lanes 0-1 and 62-63 carry the 8-column left / right halo and store
-// nothing).  No LDS and no barriers:
-//  * vertical pass in registers: the wave walks down its T + 2*6 input rows once (int4 loads of
-//    the decimated base, clamp-to-edge), and every scale's vertical sum reuses the same symmetric
+// A/B).  One wave owns a strip of output columns x T output rows of one octave; each lane holds V
+// (2 or 4) consecutive columns, and the ceil(6/V) lanes at each end of the wave carry the left /
+// right halo and store nothing.  No LDS and no barriers:
+//  * vertical pass in registers: the wave walks down its T + 2*6 input rows once (a 16-row ring
+//    of registers, 3 rows of prefetch), and every scale's vertical sum reuses the same symmetric
 //    pair sums x[i+d] + x[i-d] (taps are symmetric), so all S+3 scales cost sum(R_s + 1) FMAs;
-//  * horizontal pass across lanes: the neighbouring columns come from lanes l +- 1, l +- 2 through
-//    DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1, fused into the FMAs by the compiler);
-//  * DoG against the previous scale in registers, 960-B contiguous wave stores per level row.
+//  * horizontal pass across lanes: the neighbouring columns come from lanes l +- 1.. through DPP
+//    wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1);
+//  * DoG against the previous scale in registers, contiguous wave stores per level row.
 // Four waves per block take four vertically adjacent strips, so their shared halo rows are read
-// from L2 at the same time.  Radii are compile-time (R_s = ceil(3 sigma_s), sigma_s = 2/(s+1)); the
-// tap values come from gdp_conv_taps.
+// from L2 at the same time.  Radii and taps are compile-time constants of the scale
+// (R_s = ceil(3 sigma_s), sigma_s = 2/(s+1)); gdp_conv_taps returns the same values.
 // ------------------------------------------------------------------------------------------
-constexpr int kSwLanesOut = 60;                // lanes 2..61 produce output
-constexpr int kSwCols = 4 * kSwLanesOut;       // output columns per wave strip
-constexpr int kSwHalo = 8;                     // input columns left of the strip's first column
-constexpr int kSwWaves = 4;                    // vertically adjacent strips per block
+constexpr int kSwWaves = 4; // vertically adjacent strips per block
+// Columns per lane.  The code is generic in V; V = 2 (116-column strips, 464-B wave stores) measured
+// 1.6x slower than V = 4 (240 columns, 960-B stores) and is not instantiated.
+constexpr int kSwV = 4;
+
+template <int V>
+struct SwGeom {                                            // strip geometry for V columns per lane
+    static constexpr int kHaloLanes = (kCvR + V - 1) / V;  // lanes at each end that only load
+    static constexpr int kLanesOut = 64 - 2 * kHaloLanes;  // lanes that store
+    static constexpr int kCols = V * kLanesOut;            // output columns per strip (240 / 116)
+    static constexpr int kHalo = V * kHaloLanes;           // input columns left of the first one
+};
+template <int V>
+struct VecT;
+template <>
+struct VecT<2> {
+    typedef float f __attribute__((ext_vector_type(2)));
+    typedef int i __attribute__((ext_vector_type(2)));
+    typedef unsigned u __attribute__((ext_vector_type(2)));
+};
+template <>
+struct VecT<4> {
+    typedef float f __attribute__((ext_vector_type(4)));
+    typedef int i __attribute__((ext_vector_type(4)));
+    typedef unsigned u __attribute__((ext_vector_type(4)));
+};
 
 __host__ __device__ constexpr int conv_radius_of(int s) {
     return (6 + s) / (s + 1) > kCvR ? kCvR : ((6 + s) / (s + 1) < 1 ? 1 : (6 + s) / (s + 1));
@@ -727,46 +749,50 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// lane l receives lane l-1's (prev) / lane l+1's (next) value; the wave's end lanes receive 0
+// lane l receives lane l-1's (prev) / lane l+1's (next) value; the wave's end lanes receive 0.
+// (Measured: the exchanges cost ~1 % of the sweep — ds_bpermute instead of DPP, or no exchange
+// at all, time the same.)
 __device__ __forceinline__ float lane_prev(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true)); // wave_shr:1
 }
 __device__ __forceinline__ float lane_next(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true)); // wave_shl:1
 }
 
-// Horizontal symmetric filter of radius R over the wave-distributed row v (4 columns per lane):
-// out_j = k[0] a_j + sum_{d=1..R} k[d] (a_{j+d} + a_{j-d}), a_m = column 4l + m.
-template <int s>
-__device__ __forceinline__ f4 conv_h_lanes(f4 v) {
+// Horizontal symmetric filter of scale s over the wave-distributed row v (V columns per lane):
+// out_j = k[0] a_j + sum_{d=1..R} k[d] (a_{j+d} + a_{j-d}), a_m = column V*l + m, taken from lane
+// l - k / l + k (k = 1..ceil(R/V)) by chains of one-lane DPP shifts.
+template <int s, int V>
+__device__ __forceinline__ typename VecT<V>::f conv_h_lanes(typename VecT<V>::f v) {
     constexpr int R = conv_radius_of(s);
     constexpr ConvTaps K = conv_taps_of(s);
-    static_assert(R >= 1 && R <= 8, "radius");
-    const float c[4] = {v.x, v.y, v.z, v.w};
-    float p1[4] = {0.f, 0.f, 0.f, 0.f}, n1[4] = {0.f, 0.f, 0.f, 0.f};
-    float p2[4] = {0.f, 0.f, 0.f, 0.f}, n2[4] = {0.f, 0.f, 0.f, 0.f};
+    constexpr int KL = (R + V - 1) / V; // lanes of reach
+    float P[KL + 1][V], N[KL + 1][V];  // P[k][j] / N[k][j]: column j of lane l - k / l + k
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (j >= 4 - R) p1[j] = lane_prev(c[j]); // column 4l - 4 + j
-        if (j <= R - 1) n1[j] = lane_next(c[j]); // column 4l + 4 + j
-    }
+    for (int j = 0; j < V; ++j) P[0][j] = N[0][j] = v[j];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (R > 4 && j >= 8 - R) p2[j] = lane_prev(p1[j]); // column 4l - 8 + j
-        if (R > 4 && j <= R - 5) n2[j] = lane_next(n1[j]); // column 4l + 8 + j
-    }
+    for (int k = 1; k <= KL; ++k)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            P[k][j] = j >= V * k - R ? lane_prev(P[k - 1][j]) : 0.f;         // column V(l-k) + j
+            N[k][j] = j <= V - 1 + R - V * k ? lane_next(N[k - 1][j]) : 0.f; // column V(l+k) + j
+        }
     auto a = [&](int m) -> float {
-        return m < -4 ? p2[m + 8] : m < 0 ? p1[m + 4] : m < 4 ? c[m] : m < 8 ? n1[m - 4] : n2[m - 8];
+        if (m < 0) {
+            const int k = (-m + V - 1) / V;
+            return P[k][m + k * V];
+        }
+        return m < V ? P[0][m] : N[m / V][m % V];
     };
-    float out[4];
+    typename VecT<V>::f out;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < V; ++j) {
         float acc = K.k[0] * a(j);
 #pragma unroll
         for (int d = 1; d <= R; ++d) acc = __builtin_fmaf(K.k[d], a(j + d) + a(j - d), acc);
         out[j] = acc;
     }
-    return f4{out[0], out[1], out[2], out[3]};
+    return out;
 }
 
 // Buffer resources for the sweep: with raw buffer loads/stores every memory instruction is issued
@@ -779,55 +805,66 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
 }
 enum { kLdVecI32 = 0, kLdVecU8 = 1, kLdScalarI32 = 2, kLdScalarU8 = 3 };
 
-template <int L, int T, bool NT, int LD>
+template <int L, int T, int V, int LD>
 __device__ __forceinline__ void conv_sweep_body(const Geom* __restrict__ g, const OctGeom& og, const void* __restrict__ in,
-                                                float* __restrict__ out, int b, int o, int R0, int cin, int lane) {
+                                                float* __restrict__ out, int b, int o, int R0, int cin, int lane, int dir) {
+    typedef typename VecT<V>::f fv;
+    typedef typename VecT<V>::u uv;
     constexpr int kWin = 2 * kCvR + 1; // input rows one output row needs
     constexpr int kRing = kWin + 3;    // + 3 rows of prefetch: a 16-row register ring
     static_assert(T % kRing == 0, "strip rows must be a multiple of the ring");
     constexpr int esz = (LD == kLdVecU8 || LD == kLdScalarU8) ? 1 : 4;
     const int rows = og.rows, cols = og.cols;
     // per-lane column offsets (bytes within an input row).  Vector loads: cin and cols are
-    // multiples of 4, so a halo group is either inside the row, wholly left of it (every column
-    // clamps to column 0: broadcast .x of the group at 0) or wholly right of it (broadcast .w of
-    // the last group)
-    int voff[4];
-    const int cl = min(max(cin, 0), max(cols - 4, 0));
+    // multiples of V, so a halo group is inside the row, wholly left of it (every column clamps to
+    // column 0: broadcast [0] of the group at 0) or wholly right of it (broadcast [V-1] of the last)
+    int voff[V];
+    const int cl = min(max(cin, 0), max(cols - V, 0));
     const bool left = cin < 0, right = cin >= cols;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < V; ++j)
         voff[j] = (LD == kLdVecI32 || LD == kLdVecU8) ? cl * esz : (min(max(cin + j, 0), cols - 1) << o) * esz;
-    auto clamp_group = [&](f4 w) -> f4 {
-        const float lo = right ? w.w : w.x, hi = left ? w.x : w.w;
-        return f4{lo, left ? w.x : (right ? w.w : w.y), left ? w.x : (right ? w.w : w.z), hi};
+    auto clamp_group = [&](fv w) -> fv {
+        fv r;
+#pragma unroll
+        for (int j = 0; j < V; ++j) r[j] = left ? w[0] : (right ? w[V - 1] : w[j]);
+        return r;
     };
     const char* img = static_cast<const char*>(in) + (long long)b * g->in_img_stride * esz;
     const long long row_bytes = ((long long)g->in_pitch << o) * esz; // input bytes between octave-o rows
-    auto load = [&](int q) -> f4 {                                    // input row R0 - kCvR + q (clamped)
-        const int r = min(max(R0 - kCvR + q, 0), rows - 1);           // wave-uniform
+    // the strip is swept top-down (dir = 1) or bottom-up (dir = -1) from output row Rb
+    const int Rb = dir > 0 ? R0 : R0 + T - 1;
+    auto load = [&](int q) -> fv {                                    // input row Rb + dir (q - kCvR), clamped
+        const int r = min(max(Rb + dir * (q - kCvR), 0), rows - 1);   // wave-uniform
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(img + (long long)r * row_bytes);
+        fv x;
         if constexpr (LD == kLdVecI32) {
-            const i4 w = __builtin_bit_cast(i4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[0], 0, 0));
-            return clamp_group(__builtin_convertvector(w, f4));
+            typename VecT<V>::i w;
+            if constexpr (V == 4)
+                w = __builtin_bit_cast(typename VecT<V>::i, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[0], 0, 0));
+            else
+                w = __builtin_bit_cast(typename VecT<V>::i, __builtin_amdgcn_raw_buffer_load_b64(rs, voff[0], 0, 0));
+            return clamp_group(__builtin_convertvector(w, fv));
         } else if constexpr (LD == kLdVecU8) {
-            const unsigned w = __builtin_amdgcn_raw_buffer_load_b32(rs, voff[0], 0, 0);
-            return clamp_group(f4{(float)(w & 0xffu), (float)((w >> 8) & 0xffu), (float)((w >> 16) & 0xffu),
-                                  (float)(w >> 24)});
-        } else {
-            float x[4];
+            const unsigned w = V == 4 ? __builtin_amdgcn_raw_buffer_load_b32(rs, voff[0], 0, 0)
+                                      : (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, voff[0], 0, 0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < V; ++j) x[j] = (float)((w >> (8 * j)) & 0xffu);
+            return clamp_group(x);
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
                 if constexpr (LD == kLdScalarI32)
                     x[j] = (float)(int)__builtin_amdgcn_raw_buffer_load_b32(rs, voff[j], 0, 0);
                 else
                     x[j] = (float)__builtin_amdgcn_raw_buffer_load_b8(rs, voff[j], 0, 0);
             }
-            return f4{x[0], x[1], x[2], x[3]};
+            return x;
         }
     };
-    // one store resource per level, based at this wave's first row; lanes 0-1 / 62-63 (halo) and
-    // columns past the row end store out of range
-    const bool active = lane >= 2 && lane < 2 + kSwLanesOut && cin < cols;
+    // one store resource per level, based at this wave's first row; halo lanes and columns past the
+    // row end store out of range
+    const bool active = lane >= SwGeom<V>::kHaloLanes && lane < 64 - SwGeom<V>::kHaloLanes && cin < cols;
     const int soff_lane = active ? cin * 4 : kOOB;
     float* lev0 = out + (long long)b * g->pyr_stride + og.lev_off + (long long)R0 * cols;
     __amdgpu_buffer_rsrc_t rs_out[L];
@@ -835,49 +872,63 @@ __device__ __forceinline__ void conv_sweep_body(const Geom* __restrict__ g, cons
     for (int s = 0; s < L; ++s) rs_out[s] = make_rsrc(lev0 + (long long)s * og.lev_stride);
     // soffset stays the constant 0: with an SGPR soffset the compiler omits the wait state that a
     // VALU overwrite of a >8-byte store's data VGPRs needs right after the store, and gfx950 then
-    // stores the overwritten values (measured); the row offset goes into voffset instead
-    auto store_b128 = [&](f4 val, __amdgpu_buffer_rsrc_t rs, int vo) {
-        typedef unsigned u4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, val), rs, vo, 0, NT ? 2 : 0);
+    // stores the overwritten values (measured); the row offset goes into voffset instead.  Stores
+    // are non-temporal (nt).
+    auto store = [&](fv val, __amdgpu_buffer_rsrc_t rs, int vo) {
+        if constexpr (V == 4)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uv, val), rs, vo, 0, 2);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uv, val), rs, vo, 0, 2);
     };
-    // ring of input rows: slot q % kRing holds input row R0 - kCvR + q
-    f4 x[kRing];
+    // ring of input rows: slot q % kRing holds input row Rb + dir (q - kCvR)
+    fv x[kRing];
 #pragma unroll
     for (int q = 0; q < kRing; ++q) x[q] = load(q);
 #pragma unroll 1
-    for (int i0 = 0; i0 < T && R0 + i0 < rows; i0 += kRing) {
+    for (int i0 = 0; i0 < T && (dir < 0 || R0 + i0 < rows); i0 += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; ++u) {
-            const int i = i0 + u; // output row R0 + i needs ring slots (u + 0..12) % kRing
-            f4 pr[kCvR + 1];      // symmetric pair sums, shared by every scale
+            const int i = i0 + u; // output row Rb + dir i needs ring slots (u + 0..12) % kRing
+            const int Ri = Rb + dir * i;
+            fv pr[kCvR + 1];      // symmetric pair sums, shared by every scale
             pr[0] = x[(u + kCvR) % kRing];
 #pragma unroll
             for (int d = 1; d <= kCvR; ++d) pr[d] = x[(u + kCvR + d) % kRing] + x[(u + kCvR - d) % kRing];
             if (i + kRing < T + 2 * kCvR) x[u] = load(i + kRing); // refill the slot just used (uniform)
-            const int vo = (R0 + i < rows ? soff_lane : kOOB) + i * cols * 4; // OOB stays OOB (< 2^32)
-            f4 hprev = {0.f, 0.f, 0.f, 0.f};
+            const int vo = (Ri < rows ? soff_lane : kOOB) + (Ri - R0) * cols * 4; // OOB stays OOB (< 2^32)
+            fv hprev = {};
             static_for<L>([&](auto si) {
                 constexpr int s = decltype(si)::value;
                 constexpr int R = conv_radius_of(s);
                 constexpr ConvTaps K = conv_taps_of(s);
-                f4 vs = pr[0] * K.k[0];
+                fv vs = pr[0] * K.k[0];
 #pragma unroll
-                for (int d = 1; d <= R; ++d) vs = fma4(K.k[d], pr[d], vs);
-                const f4 h = conv_h_lanes<s>(vs);
-                if constexpr (s > 0) store_b128(hprev - h, rs_out[s - 1], vo);
+                for (int d = 1; d <= R; ++d) vs = __builtin_elementwise_fma((fv)K.k[d], pr[d], vs);
+                const fv h = conv_h_lanes<s, V>(vs);
+                if constexpr (s > 0) store(hprev - h, rs_out[s - 1], vo);
                 hprev = h;
             });
-            store_b128(hprev, rs_out[L - 1], vo);
+            store(hprev, rs_out[L - 1], vo);
+            __builtin_amdgcn_sched_barrier(0); // keep each row's loads in its own row: no hoisting into spills
         }
     }
 }
 
-template <int L, int T, bool NT>
-__global__ void __launch_bounds__(64 * kSwWaves, 4) k_conv_sweep(const Geom* __restrict__ g, const void* __restrict__ in,
-                                                                 float* __restrict__ out) {
+template <int L, int T, int V>
+__global__ void __launch_bounds__(64 * kSwWaves, V == 4 ? 4 : 6) k_conv_sweep(const Geom* __restrict__ g,
+                                                                              const void* __restrict__ in,
+                                                                              float* __restrict__ out, unsigned units,
+                                                                              int order) {
+    // order 1 (XCD-chunked): blocks u and u+8 share an XCD under round-robin dispatch, so XCD x
+    // takes the contiguous work range x/8 — horizontally adjacent strips of a row band then run
+    // on one XCD at the same time and their shared boundary lines meet in one L2 (the grid is
+    // padded to a multiple of 8; the padding blocks exit)
+    unsigned w = blockIdx.x;
+    if (order & 1) w = (w & 7u) * (gridDim.x >> 3) + (w >> 3);
+    if (w >= units) return;
     const unsigned per = g->sw_blk[g->O];
-    const unsigned b = blockIdx.x / per;
-    const unsigned v = blockIdx.x - b * per;
+    const unsigned b = w / per;
+    const unsigned v = w - b * per;
     int o = 0;
     while (o + 1 < g->O && v >= g->sw_blk[o + 1]) ++o;
     const OctGeom og = g->oct[o];
@@ -888,16 +939,19 @@ __global__ void __launch_bounds__(64 * kSwWaves, 4) k_conv_sweep(const Geom* __r
     const int lane = threadIdx.x & 63;
     const int R0 = (tr * kSwWaves + wave) * T; // first output row of this wave
     if (R0 >= og.rows) return;                 // whole waves only; no barriers in this kernel
-    const int cin = tc * kSwCols - kSwHalo + 4 * lane;
+    const int cin = tc * SwGeom<V>::kCols - SwGeom<V>::kHalo + V * lane;
+    // order bit 1: odd waves sweep bottom-up, so every halo shared by two waves of the block is
+    // loaded by both at the same time (ends meet ends, starts meet starts) and hits in cache
+    const int dir = (order & 2) && (wave & 1) ? -1 : 1;
     if (o == 0 && g->vec_in && og.cols >= 4) {
         if (g->in_fmt == GDP_INPUT_U8)
-            conv_sweep_body<L, T, NT, kLdVecU8>(g, og, in, out, (int)b, o, R0, cin, lane);
+            conv_sweep_body<L, T, V, kLdVecU8>(g, og, in, out, (int)b, o, R0, cin, lane, dir);
         else
-            conv_sweep_body<L, T, NT, kLdVecI32>(g, og, in, out, (int)b, o, R0, cin, lane);
+            conv_sweep_body<L, T, V, kLdVecI32>(g, og, in, out, (int)b, o, R0, cin, lane, dir);
     } else if (g->in_fmt == GDP_INPUT_U8) {
-        conv_sweep_body<L, T, NT, kLdScalarU8>(g, og, in, out, (int)b, o, R0, cin, lane);
+        conv_sweep_body<L, T, V, kLdScalarU8>(g, og, in, out, (int)b, o, R0, cin, lane, dir);
     } else {
-        conv_sweep_body<L, T, NT, kLdScalarI32>(g, og, in, out, (int)b, o, R0, cin, lane);
+        conv_sweep_body<L, T, V, kLdScalarI32>(g, og, in, out, (int)b, o, R0, cin, lane, dir);
     }
 }
 
@@ -1018,6 +1072,7 @@ struct gdp_ctx {
     float* d_taps = nullptr;
     int conv_kernel = 0;          // GDP_TUNE_CONV_KERNEL: 0 register sweep (default), 1 LDS tiles
     int conv_rows = 16;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep
+    int conv_order = 0;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
     int* d_cradius = nullptr;     // convolution-mode radius per scale
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
@@ -1155,12 +1210,13 @@ bool valid_level(const gdp_ctx* c, int b, int o, int s) {
 // Block prefix of the convolution sweep (kSwWaves strips of conv_rows rows x kSwCols columns).
 static void conv_sweep_geom(gdp_ctx* c) {
     Geom& g = c->geom;
+    const int strip_cols = SwGeom<kSwV>::kCols;
     g.sw_blk[0] = 0;
     g.cvx_blk[0] = 0;
     for (int o = 0; o < g.O; ++o) {
         const OctGeom& og = g.oct[o];
-        const bool sweep = og.cols >= 4 && og.cols % 4 == 0; // full 16-B stores on every row
-        g.sw_strips_c[o] = (og.cols + kSwCols - 1) / kSwCols;
+        const bool sweep = og.cols >= 4 && og.cols % 4 == 0; // full-vector stores on every row
+        g.sw_strips_c[o] = (og.cols + strip_cols - 1) / strip_cols;
         const long long rows_per_blk = (long long)kSwWaves * c->conv_rows;
         g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
         g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
@@ -1168,19 +1224,16 @@ static void conv_sweep_geom(gdp_ctx* c) {
 }
 
 template <int L, int T>
-hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned grid, hipStream_t st) {
-    auto k = c->nontemporal ? k_conv_sweep<L, T, true> : k_conv_sweep<L, T, false>;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kSwWaves), 0, st, c->d_geom, c->d_in, c->d_out);
+hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
+    auto k = k_conv_sweep<L, T, kSwV>;
+    const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kSwWaves), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order);
     return hipGetLastError();
 }
 
 template <int L>
 hipError_t launch_conv_sweep_l(gdp_ctx* c, unsigned grid, hipStream_t st) {
-    switch (c->conv_rows) {
-        case 32: return launch_conv_sweep_t<L, 32>(c, grid, st);
-        case 64: return launch_conv_sweep_t<L, 64>(c, grid, st);
-        default: return launch_conv_sweep_t<L, 16>(c, grid, st);
-    }
+    return c->conv_rows == 32 ? launch_conv_sweep_t<L, 32>(c, grid, st) : launch_conv_sweep_t<L, 16>(c, grid, st);
 }
 
 extern "C" {
@@ -1524,7 +1577,7 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) {
     const bool sweep = c->conv_kernel == 0 && g.L >= 3 && g.L <= 6;
     if (sweep) {
         const long long grid = (long long)g.sw_blk[g.O] * g.batch;
-        if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
+        if (grid >= (1ll << 31) - 8) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
         if (grid > 0) {
             switch (g.L) {
                 case 3: GDP_HIP(c, launch_conv_sweep_l<3>(c, (unsigned)grid, st)); break;
@@ -1761,6 +1814,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_WINDOW_SUB: *value = c->window_sub; return GDP_OK;
         case GDP_TUNE_CONV_KERNEL: *value = c->conv_kernel; return GDP_OK;
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
+        case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 }
@@ -1790,7 +1844,7 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             c->conv_kernel = value;
             return GDP_OK;
         case GDP_TUNE_CONV_ROWS: {
-            if (value != 16 && value != 32 && value != 64) return c->status(GDP_ERR_ARG, "conv rows must be 16, 32 or 64");
+            if (value != 16 && value != 32) return c->status(GDP_ERR_ARG, "conv rows must be 16 or 32");
             const int old = c->conv_rows;
             c->conv_rows = value;
             conv_sweep_geom(c);
@@ -1801,6 +1855,10 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             }
             return rc;
         }
+        case GDP_TUNE_CONV_ORDER:
+            if (value < 0 || value > 3) return c->status(GDP_ERR_ARG, "conv order must be 0..3");
+            c->conv_order = value;
+            return GDP_OK;
         case GDP_TUNE_TILE_ORDER:
             if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");
             c->geom.tile_order = value;

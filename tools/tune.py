@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv"])
     ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
+    ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
     args = ap.parse_args()
     pkg = entry.load_package()
@@ -45,7 +46,8 @@ def main():
         variants.append((v, {"nontemporal": int(kv.get("nt", 1)), "grid": int(kv.get("grid", "0"), 0),
                              "variant": int(kv.get("v", -1)) if "v" in kv else None,
                              "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1)),
-                             "conv_kernel": int(kv.get("ck", 0)), "conv_rows": int(kv.get("cr", 16))}))
+                             "conv_kernel": int(kv.get("ck", 0)), "conv_rows": int(kv.get("cr", 16)),
+                             "conv_order": int(kv.get("co", 0))}))
         if variants[-1][1]["variant"] is None:
             del variants[-1][1]["variant"]
         if "bpc" in kv:
@@ -66,7 +68,9 @@ def main():
         lev = ctx.level(0, 0, 0)
         if ref is None:
             ref = lev
-        if args.op == "conv":  # the two convolution kernels round differently (no parity contract)
+        if args.no_check:
+            pass
+        elif args.op == "conv":  # the two convolution kernels round differently (no parity contract)
             assert np.allclose(lev, ref, rtol=1e-5, atol=1e-3), name
         else:
             assert np.array_equal(lev.view(np.uint32), ref.view(np.uint32)), name
