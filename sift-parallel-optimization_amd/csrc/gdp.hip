@@ -92,6 +92,7 @@ struct Geom {
     unsigned tail_groups_per_img, tail_units;  // octaves >= F, 256 groups per unit
     OctGeom oct[kMaxOct];
     unsigned lv_blk[kMaxOct + 1]; // prefix over octaves of ceil(rows*gpr / kLevBlock) per image
+    unsigned lx_blk[kMaxOct + 1]; // prefix over octaves of ceil(rows*gpr / 64) per image (k_levels_x)
     unsigned cv_blk[kMaxOct + 1]; // convolution mode: prefix over octaves of 16x256 output tiles
     int cv_tiles_c[kMaxOct];      // convolution mode: tile columns per octave
     unsigned sw_blk[kMaxOct + 1]; // convolution sweep: prefix over octaves of blocks (4 strips of T rows);
@@ -492,6 +493,65 @@ __global__ void __launch_bounds__(kLevBlock / SUB) k_window(const Geom* __restri
         if (n > 2) r.z = p[2];
         if (n > 3) r.w = p[3];
         st_part(p, (r * fc) * fr, n, false);
+    }
+}
+
+// DoG / GenerateDoG re-entry (MODE 2 / 3) with one LEVEL per wave: a block of 64 x L threads
+// takes 64 four-pixel groups; wave s loads level s (one float4 per lane, like k_window), applies
+// the window of scale s (MODE 3), parks the result in LDS, and after one barrier forms
+// out_s = G_s - G_{s+1} from its own value and wave s+1's; level L-1 keeps G (MODE 3) or is left
+// untouched (MODE 2).  In place is safe: every value a wave needs from another level is read
+// (into LDS) before the barrier, every store happens after it, and blocks own disjoint pixels.
+template <int MODE, bool NT>
+__global__ void __launch_bounds__(1024) k_levels_x(const Geom* __restrict__ g, float* __restrict__ out,
+                                                   const float* __restrict__ taps, int o_begin, int o_end) {
+    __shared__ f4 xs[16][64];
+    const unsigned first = g->lx_blk[o_begin];
+    const unsigned per = g->lx_blk[o_end] - first;
+    const unsigned b = blockIdx.x / per;
+    const unsigned v = blockIdx.x - b * per + first;
+    int o = o_begin;
+    while (o + 1 < o_end && v >= g->lx_blk[o + 1]) ++o;
+    const OctGeom og = g->oct[o];
+    const int L = g->L;
+    const int s = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const unsigned k = (v - g->lx_blk[o]) * 64u + (unsigned)lane;
+    const bool valid = k < (unsigned)og.rows * (unsigned)og.gpr;
+    int Rl = 0, C = 0, n = 0;
+    float* p = nullptr;
+    f4 gs = {0.f, 0.f, 0.f, 0.f};
+    bool full = false;
+    if (valid) {
+        Rl = (int)fast_div(k, og.gpr_magic, og.gpr_shift);
+        C = 4 * (int)(k - (unsigned)Rl * (unsigned)og.gpr);
+        n = min(4, og.cols - C);
+        full = (n == 4) && ((og.cols & 3) == 0);
+        p = out + (long long)b * g->pyr_stride + og.lev_off + (long long)s * og.lev_stride + (long long)Rl * og.cols + C;
+        if (full) {
+            gs = ld_stream<NT>(p);
+        } else {
+            gs.x = p[0];
+            if (n > 1) gs.y = p[1];
+            if (n > 2) gs.z = p[2];
+            if (n > 3) gs.w = p[3];
+        }
+        if constexpr ((MODE & 1) != 0)
+            gs = (gs * ld_f4(taps + og.ctap + s * og.ctap_stride + C)) * taps[og.rtap + s * og.rtap_stride + og.row0 + Rl];
+    }
+    xs[s][lane] = gs;
+    __syncthreads();
+    if (!valid) return;
+    if (s + 1 < L) {
+        const f4 d = gs - xs[s + 1][lane];
+        if (full)
+            st_f4<NT>(p, d);
+        else
+            st_part(p, d, n, false);
+    } else if constexpr ((MODE & 1) != 0) {
+        if (full)
+            st_f4<NT>(p, gs);
+        else
+            st_part(p, gs, n, false);
     }
 }
 
@@ -1191,6 +1251,16 @@ int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st) {
 
 template <int MODE>
 int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
+    const Geom& g = c->geom;
+    if ((MODE == 2 || MODE == 3) && c->inplace_sub == 0 && g.L <= 16) {
+        const long long grid = ((long long)g.lx_blk[oe] - g.lx_blk[ob]) * g.batch;
+        if (grid <= 0) return GDP_OK;
+        if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "in-place pass too large for one launch");
+        auto kern = c->nontemporal ? k_levels_x<MODE == 3 ? 3 : 2, true> : k_levels_x<MODE == 3 ? 3 : 2, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * g.L), 0, st, c->d_geom, c->d_out, c->d_taps, ob, oe);
+        GDP_HIP(c, hipGetLastError());
+        return GDP_OK;
+    }
     switch (MODE == 1 ? c->window_sub : c->inplace_sub) {
         case 2: return launch_inplace_sub<MODE, 2>(c, ob, oe, st);
         case 4: return launch_inplace_sub<MODE, 4>(c, ob, oe, st);
@@ -1336,6 +1406,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         make_magic((unsigned)std::max(1, og.gpr), &og.gpr_magic, &og.gpr_shift);
         grp += (long long)og.rows * og.gpr;
         g.lv_blk[o + 1] = g.lv_blk[o] + (unsigned)(((long long)og.rows * og.gpr + kLevBlock - 1) / kLevBlock);
+        g.lx_blk[o + 1] = g.lx_blk[o] + (unsigned)(((long long)og.rows * og.gpr + 63) / 64);
         g.cv_tiles_c[o] = (og.cols + kCvTW - 1) / kCvTW;
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
@@ -1836,7 +1907,8 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             return GDP_OK;
         case GDP_TUNE_INPLACE_SUB:
         case GDP_TUNE_WINDOW_SUB:
-            if (value != 1 && value != 2 && value != 4) return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4");
+            if ((value != 1 && value != 2 && value != 4) && !(key == GDP_TUNE_INPLACE_SUB && value == 0))
+                return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4 (in-place DoG also 0: one level per wave)");
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
         case GDP_TUNE_CONV_KERNEL:

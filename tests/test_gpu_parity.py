@@ -255,11 +255,13 @@ def test_int_star_star_upload(pkg, oracle):
 
 
 # ------------------------------------------------------------------ in-place ops / re-entry
-def test_inplace_ops_match_reference_order(pkg, oracle):
+@pytest.mark.parametrize("sub", [0, 1])
+def test_inplace_ops_match_reference_order(pkg, oracle, sub):
     H, W, S = 72, 104, 2
     O = oracle.default_octaves(H, W)
     img = oracle.lcg_image(H, W, 21)
     with pkg.PyramidContext(H, W, S=S) as ctx:
+        ctx.set_tuning(inplace_sub=sub)
         ctx.set_input(img)
         ctx.init()
         want = oracle.init_pyramid(img, S)
@@ -276,15 +278,16 @@ def test_inplace_ops_match_reference_order(pkg, oracle):
         _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
 
 
-@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4)])
+@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0)])
 def test_gauss_range_and_store_modes(pkg, oracle, nt, sub):
     """One-launch GaussFilter over an octave range == per-octave GaussFilter; both store modes;
-    a batch of 3 and a generic-S (S = 4) context."""
-    for H, W, S, B in [(90, 200, 2, 3), (64, 48, 4, 1)]:
+    every in-place DoG kernel (sub 0 = one level per wave, k_levels_x; S = 14 has 17 levels and
+    falls back to k_levels); a batch of 3 and generic-S contexts."""
+    for H, W, S, B in [(90, 200, 2, 3), (64, 48, 4, 1), (40, 36, 14, 1)]:
         O = oracle.default_octaves(H, W)
         imgs = [oracle.lcg_image(H, W, 5 + b) for b in range(B)]
         with pkg.PyramidContext(H, W, S=S, batch=B) as ctx:
-            ctx.set_tuning(nontemporal=nt, inplace_sub=sub, window_sub=4 // sub)
+            ctx.set_tuning(nontemporal=nt, inplace_sub=sub, window_sub=4 // max(sub, 1))
             for b, img in enumerate(imgs):
                 ctx.set_input(img, b)
             ctx.init()
