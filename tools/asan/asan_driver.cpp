@@ -1,0 +1,119 @@
+// Host-side AddressSanitizer / UBSan run of the C ABI (GPU kernels are not instrumented: only
+// -Xarch_host gets -fsanitize).  Exercises every export on small shapes, including the error paths,
+// and checks a few invariants (fused build == GaussPyInit + GenerateDoG by checksum, downloads
+// agree with each other).  Build + run on the GPU box:  make -C tools/asan run
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "gdp.h"
+
+static int failures = 0;
+#define EXPECT(cond)                                                                  \
+    do {                                                                              \
+        if (!(cond)) {                                                                \
+            std::fprintf(stderr, "%s:%d: expectation failed: %s\n", __FILE__, __LINE__, #cond); \
+            ++failures;                                                               \
+        }                                                                             \
+    } while (0)
+#define OK(call) EXPECT((call) == GDP_OK)
+
+static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
+    gdp_ctx* c = nullptr;
+    const bool band = r1 > r0;
+    OK(band ? gdp_create_band(&c, H, W, S, O, B, r0, r1, 0) : gdp_create(&c, H, W, S, O, B, 0));
+    if (!c) return;
+    int gh, gw, gs, go, gb, rows, cols0, first0;
+    OK(gdp_get_geometry(c, &gh, &gw, &gs, &go, &gb));
+    OK(gdp_level_dims(c, 0, &rows, &cols0, &first0)); // input rows held = octave-0 rows
+    std::vector<int32_t> img((size_t)rows * W);
+    for (size_t i = 0; i < img.size(); ++i) img[i] = (int32_t)((i * 2654435761u) >> 24);
+    std::vector<const int32_t*> rowp(rows);
+    for (int r = 0; r < rows; ++r) rowp[r] = img.data() + (size_t)r * W;
+    for (int b = 0; b < gb; ++b) {
+        OK(gdp_set_input_host(c, b, img.data(), (size_t)W, nullptr));
+        OK(gdp_set_input_rows(c, b, rowp.data(), nullptr));
+    }
+    OK(gdp_build(c, nullptr));
+    OK(gdp_sync(c));
+    uint64_t built = 0, again = 0;
+    OK(gdp_checksum(c, 0, &built));
+    OK(gdp_init(c, nullptr));
+    OK(gdp_generate_dog(c, nullptr));
+    OK(gdp_checksum(c, 0, &again));
+    EXPECT(built == again);
+    for (int o = 0; o < go; ++o) {
+        int lr, lc, first;
+        OK(gdp_level_dims(c, o, &lr, &lc, &first));
+        std::vector<float> dense((size_t)lr * lc + 1), range((size_t)lr * lc + 1);
+        std::vector<std::vector<float>> rws(lr, std::vector<float>(lc));
+        std::vector<float*> rp(lr);
+        for (int r = 0; r < lr; ++r) rp[r] = rws[r].data();
+        for (int s = 0; s < gs + 3; ++s) {
+            OK(gdp_download_level(c, 0, o, s, dense.data()));
+            OK(gdp_download_level_rows(c, 0, o, s, rp.data()));
+            OK(gdp_download_level_range(c, 0, o, s, 0, lr, range.data()));
+            for (int r = 0; r < lr; ++r) {
+                EXPECT(std::memcmp(rws[r].data(), dense.data() + (size_t)r * lc, (size_t)lc * 4) == 0);
+                EXPECT(std::memcmp(range.data() + (size_t)r * lc, dense.data() + (size_t)r * lc, (size_t)lc * 4) == 0);
+            }
+            EXPECT(gdp_download_level_range(c, 0, o, s, lr, 1, range.data()) != GDP_OK);
+        }
+        OK(gdp_gauss_octave(c, o, nullptr));
+        OK(gdp_dog_octave(c, o, nullptr));
+    }
+    std::vector<float> packed(gdp_packed_floats(c));
+    OK(gdp_download_pyramid(c, 0, packed.data()));
+    OK(gdp_upload_pyramid(c, 0, packed.data()));
+    OK(gdp_gauss_range(c, 0, go, nullptr));
+    // tuning: every key, valid and invalid values
+    for (int key = 1; key <= 11; ++key) {
+        int v = -1;
+        if (gdp_get_tuning(c, key, &v) == GDP_OK) OK(gdp_set_tuning(c, key, v));
+    }
+    EXPECT(gdp_set_tuning(c, GDP_TUNE_VARIANT, 99) != GDP_OK);
+    EXPECT(gdp_set_tuning(c, GDP_TUNE_CONV_ROWS, 7) != GDP_OK);
+    EXPECT(gdp_set_tuning(c, 12345, 0) != GDP_OK);
+    for (int v = 0; v < 9; ++v) OK(gdp_set_tuning(c, GDP_TUNE_VARIANT, v));
+    int bv = -1, bo = -1;
+    float bms = 0;
+    OK(gdp_autotune(c, 1, nullptr, &bv, &bo, &bms));
+    float ms = 0;
+    OK(gdp_time_builds(c, 2, nullptr, &ms));
+    if (!band) {
+        OK(gdp_build_gaussian(c, nullptr));
+        OK(gdp_set_tuning(c, GDP_TUNE_CONV_KERNEL, 1));
+        OK(gdp_build_gaussian(c, nullptr));
+    } else {
+        EXPECT(gdp_build_gaussian(c, nullptr) != GDP_OK);
+    }
+    OK(gdp_fill_synthetic(c, 0x5EED, 3, nullptr));
+    OK(gdp_set_input_format(c, GDP_INPUT_U8));
+    std::vector<uint8_t> u8((size_t)rows * W, 7);
+    OK(gdp_set_input_host_u8(c, 0, u8.data(), (size_t)W, nullptr));
+    OK(gdp_build(c, nullptr));
+    float tap[4096];
+    OK(gdp_get_taps(c, 0, 0, 0, tap));
+    EXPECT(gdp_get_taps(c, 2, 0, 0, tap) != GDP_OK);
+    EXPECT(gdp_device_level(c, 0, go, 0) == nullptr);
+    OK(gdp_sync(c));
+    gdp_destroy(c);
+}
+
+int main() {
+    std::setvbuf(stdout, nullptr, _IONBF, 0);
+    EXPECT(gdp_device_count() >= 1);
+    exercise(96, 160, 2, 0, 1, 0, 0);
+    exercise(100, 37, 3, 0, 2, 0, 0);
+    exercise(7, 5, 0, 0, 1, 0, 0);
+    exercise(256, 300, 2, 5, 1, 16, 48);
+    exercise(1080, 1920, 2, 5, 1, 0, 0);
+    gdp_ctx* c = nullptr;
+    EXPECT(gdp_create(&c, 0, 10, 2, 0, 1, 0) != GDP_OK);
+    EXPECT(gdp_create(&c, 10, 10, 2, 9, 1, 0) != GDP_OK);
+    EXPECT(gdp_create_band(&c, 64, 64, 2, 5, 1, 3, 40, 0) != GDP_OK);
+    gdp_destroy(nullptr);
+    std::printf(failures ? "asan driver: %d failures\n" : "asan driver: ok\n", failures);
+    return failures ? 1 : 0;
+}
