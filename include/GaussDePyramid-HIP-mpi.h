@@ -77,11 +77,7 @@ protected:
             std::abort();
         }
     }
-    void sync_host_() {
-        for (int o = 0; o < layer; ++o)
-            for (int s = 0; s < S + 3; ++s)
-                check_(gdp_download_level_rows(full_, 0, o, s, GaussPy[o][s]), "download", full_);
-    }
+    void sync_host_() { check_(gdp_download_pyramid_rows(full_, 0, GaussPy), "download", full_); }
 };
 
 inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi()

@@ -63,9 +63,7 @@ void GaussPyInit(int* data[MAX]) {
     is_initialized = true;
     gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
     gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
-    for (int o = 0; o < layer; ++o)
-        for (int s = 0; s < S + 3; ++s)
-            gdp_mpitest_check(gdp_download_level_rows(gdp_mpitest_ctx, 0, o, s, GaussPy[o][s]), "GaussPyInit");
+    gdp_mpitest_check(gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy), "GaussPyInit");
     gdp_mpitest_fresh = true;
 }
 
@@ -75,9 +73,7 @@ static inline void gdp_mpitest_generate() {
                       "GenerateDoG_mpi");
     gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");
     gdp_mpitest_fresh = false;
-    for (int o = 0; o < layer; ++o)
-        for (int s = 0; s < S + 3; ++s)
-            gdp_mpitest_check(gdp_download_level_rows(gdp_mpitest_ctx, 0, o, s, GaussPy[o][s]), "GenerateDoG_mpi");
+    gdp_mpitest_check(gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy), "GenerateDoG_mpi");
     auto end = std::chrono::steady_clock::now();
     std::cout << std::chrono::duration<double>(end - begin).count() << std::endl;
 }

@@ -96,10 +96,8 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
     GaussPyInit();
 }
 
-inline void GaussPyramid_hip::SyncHost() {
-    for (int o = 0; o < layer; ++o)
-        for (int s = 0; s < S + 3; ++s)
-            check_(ctx_, gdp_download_level_rows(ctx_, 0, o, s, GaussPy[o][s]), "SyncHost");
+inline void GaussPyramid_hip::SyncHost() {  // one staged copy + one sync per 64 MiB, not one per level
+    check_(ctx_, gdp_download_pyramid_rows(ctx_, 0, GaussPy), "SyncHost");
 }
 
 inline void GaussPyramid_hip::GaussPyInit() {

@@ -151,6 +151,11 @@ int gdp_download_level(gdp_ctx* ctx, int b, int octave, int scale, float* host);
 /* Copy level (o, s) of image b into host row pointers — materialises the reference's
  * float**** GaussPy[o][s] rows (GuassDePyramid.h:16) (blocking). */
 int gdp_download_level_rows(gdp_ctx* ctx, int b, int octave, int scale, float* const* rows);
+/* Mirror image b's whole pyramid into the reference's host layout GaussPy[o][s][row] (the
+ * float**** of GuassDePyramid.h:16; rows as held by this context), staging every level through
+ * one pinned buffer with one stream sync per 64 MiB (blocking).  What the drop-in classes call
+ * after each mutating method. */
+int gdp_download_pyramid_rows(gdp_ctx* ctx, int b, float* const* const* const* gauss_py);
 /* Copy rows [first_row, first_row + nrows) of level (o, s) of image b (rows as held by this
  * context; a band context's row 0 is its first row) to a dense host array (blocking).  Reads one
  * GaussPy[o][s][r] row range without materialising the level (e.g. 65536^2 images). */

@@ -69,6 +69,7 @@ SIGNATURES = {
     "gdp_download_level": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_download_level_rows": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_download_level_range": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _p]),
+    "gdp_download_pyramid_rows": (_c_int, [_p, _c_int, _p]),
     "gdp_download_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_upload_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_packed_floats": (_c_size, [_p]),

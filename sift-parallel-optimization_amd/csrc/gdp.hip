@@ -1738,6 +1738,63 @@ int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows)
     return GDP_OK;
 }
 
+int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py) {
+    if (!c || !py || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid_rows: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    const Geom& g = c->geom;
+    // levels are gathered into one pinned staging buffer (<= kStageFloats, or one level) with one
+    // stream sync per fill, then scattered into the caller's rows; a level larger than the
+    // staging buffer goes through the row-chunked gdp_download_level_rows
+    size_t cap = 0;
+    for (int o = 0; o < g.O; ++o) cap += (size_t)g.oct[o].rows * g.oct[o].cols * g.L;
+    cap = std::min(cap, kStageFloats);
+    if (cap == 0) return GDP_OK;
+    if (c->h_stage_floats < cap) {
+        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->h_stage_floats = 0;
+        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, cap * 4, hipHostMallocDefault));
+        c->h_stage_floats = cap;
+    }
+    struct Pending { int o, s; size_t off; };
+    std::vector<Pending> pend;
+    size_t used = 0;
+    auto flush = [&]() -> int {
+        if (pend.empty()) return GDP_OK;
+        GDP_HIP(c, hipStreamSynchronize(c->stream));
+        for (const Pending& q : pend) {
+            const OctGeom& og = g.oct[q.o];
+            for (int r = 0; r < og.rows; ++r)
+                std::memcpy(py[q.o][q.s][r], c->h_stage + q.off + (size_t)r * og.cols, (size_t)og.cols * 4);
+        }
+        pend.clear();
+        used = 0;
+        return GDP_OK;
+    };
+    for (int o = 0; o < g.O; ++o) {
+        const OctGeom& og = g.oct[o];
+        const size_t n = (size_t)og.rows * og.cols;
+        for (int s = 0; s < g.L && n; ++s) {
+            if (n > c->h_stage_floats) {  // does not fit: row-chunked path
+                int rc = flush();
+                if (rc == GDP_OK) rc = gdp_download_level_rows(c, b, o, s, py[o][s]);
+                if (rc != GDP_OK) return rc;
+                continue;
+            }
+            if (used + n > c->h_stage_floats) {
+                const int rc = flush();
+                if (rc != GDP_OK) return rc;
+            }
+            GDP_HIP(c, hipMemcpyAsync(c->h_stage + used, gdp_device_level(c, b, o, s), n * 4, hipMemcpyDeviceToHost,
+                                      c->stream));
+            pend.push_back({o, s, used});
+            used += n;
+        }
+    }
+    return flush();
+}
+
 int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int nrows, float* host) {
     if (!valid_level(c, b, o, s) || !host || first_row < 0 || nrows < 0 || first_row > c->geom.oct[o].rows ||
         nrows > c->geom.oct[o].rows - first_row)

@@ -404,6 +404,41 @@ def test_row_downloads_chunked_and_ranged(pkg, oracle):
             ctx.level_range(0, 0, 0, n - 1, 2)
 
 
+def test_pyramid_rows_mirror(pkg, oracle):
+    """gdp_download_pyramid_rows (one staged copy into the reference's float**** GaussPy layout)
+    == the packed download, for a whole image, a batch image and a row band."""
+    import ctypes
+
+    from sift_parallel_optimization_amd import _lib
+
+    for H, W, S, B, band in [(96, 160, 2, 1, None), (100, 37, 3, 2, None), (256, 300, 2, 1, (16, 48))]:
+        kw = dict(row_begin=band[0], row_end=band[1]) if band else {}
+        with pkg.PyramidContext(H, W, S=S, batch=B, octaves=5 if band else 0, **kw) as ctx:
+            ctx.fill_synthetic(0x5EED, 2)
+            ctx.build()
+            b = B - 1
+            rows = {}
+            top = (ctypes.c_void_p * ctx.O)()
+            keep = []
+            for o in range(ctx.O):
+                nr, nc, _ = ctx.level_dims(o)
+                lev = (ctypes.c_void_p * (S + 3))()
+                for s in range(S + 3):
+                    arrs = [np.full(nc, np.nan, np.float32) for _ in range(max(nr, 1))]
+                    rows[(o, s)] = arrs[:nr]
+                    rp = (ctypes.c_void_p * max(nr, 1))(*[a.ctypes.data for a in arrs])
+                    keep.append((arrs, rp))
+                    lev[s] = ctypes.cast(rp, ctypes.c_void_p)
+                keep.append(lev)
+                top[o] = ctypes.cast(lev, ctypes.c_void_p)
+            _lib.check(_lib.lib().gdp_download_pyramid_rows(ctx._ctx, b, top), ctx._ctx)
+            for o in range(ctx.O):
+                for s in range(S + 3):
+                    want = ctx.level(b, o, s)
+                    got = np.stack(rows[(o, s)]) if rows[(o, s)] else want
+                    _assert_same(got, want, ("mirror", H, W, o, s))
+
+
 def test_max_size_65536_all_octaves(pkg, oracle):
     """The largest square image one MI355X holds with its whole pyramid resident: 65536^2 = 2^32
     input pixels (every pixel index past 32 bits), all 17 octaves (octaves >= 5 as tail units):
