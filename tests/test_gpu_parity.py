@@ -549,6 +549,10 @@ def test_cpp_dropin_driver_matches_reference(oracle, golden, tmp_path):
             assert oracle.fnv(lv[(o, s)]) == int(h, 16), (o, s)
     subprocess.run([exe, "64", "2", "lcg:12345", str(out), "3"], check=True, timeout=120)
     _assert_same(np.fromfile(out, dtype=np.float32), golden["dumps"]["regen_64_2_lcg-12345_3"], "driver regen x3")
+    for n, S in [(1, 2), (3, 0), (100, 3)]:  # degenerate and odd sizes through the drop-in class
+        subprocess.run([exe, str(n), str(S), "lcg:12345", str(out), "1"], check=True, timeout=120)
+        _assert_same(np.fromfile(out, dtype=np.float32),
+                     oracle.build_pyramid(oracle.image_from_spec(n, "lcg:12345"), S), ("driver", n, S))
     timing = subprocess.run([exe], check=True, timeout=120, capture_output=True, text=True).stdout.splitlines()
     assert len(timing) == 2 and all(float(t.split()[0]) > 0 for t in timing), timing
 
