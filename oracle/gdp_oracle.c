@@ -112,8 +112,9 @@ void gdo_build(const int32_t* img, int H, int W, long pitch, int S, int O, float
 }
 
 /*
- * One row of every level of octave o — the closed form above restricted to level row r, for
- * checking sampled rows of images too large to restate whole (65536^2: 114 GB of pyramid).
+ * One row of every level of octave o — the closed form above (GuassDePyramid.h:76-86 refill,
+ * :122-131 row then column window, :140-146 DoG) restricted to level row r, for checking sampled
+ * rows of images too large to restate whole (65536^2: 114 GB of pyramid).
  * in_row = input row r << o (W int32); out = [S+3][W >> o]; taps scratch >= 2*(S+3)*max(H,W).
  */
 void gdo_level_row(const int32_t* in_row, int H, int W, int S, int o, int r, float* out, float* taps) {
@@ -259,7 +260,7 @@ static uint32_t gdo_mix32(uint32_t x) {
     return x;
 }
 
-/* Row r of gdo_synthetic_image (W int32). */
+/* Row r of gdo_synthetic_image (W int32): the same counter hash. */
 void gdo_synthetic_row(int32_t* row, int H, int W, uint32_t seed, long image_index, long r) {
     for (long c = 0; c < W; ++c) {
         const uint64_t idx = ((uint64_t)image_index * (uint64_t)H + (uint64_t)r) * (uint64_t)W + (uint64_t)c;
