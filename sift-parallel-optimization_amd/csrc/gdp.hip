@@ -352,9 +352,19 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         og.ctap_stride = (int)round_up(og.cols, 4);
         og.ctap = (int)tap_off;
         tap_off += (long long)og.ctap_stride * g.L;
-        og.rtap_stride = (int)round_up(Hg, 4);
-        og.rtap = (int)tap_off;
-        tap_off += (long long)og.rtap_stride * g.L;
+        // Row taps.  A square image's row and column windows are the same array (host_taps of
+        // the same length), so its row taps alias the column taps: those stay hot in L2 (every
+        // tile row re-reads them), while a separate row-tap array is touched once per tile row and
+        // misses cold on every octave of every tile of a large image (measured: 16384^2 1.41 ->
+        // 1.28 ms).  Bit-identical either way.
+        if (H == W) {
+            og.rtap_stride = og.ctap_stride;
+            og.rtap = og.ctap;
+        } else {
+            og.rtap_stride = (int)round_up(Hg, 4);
+            og.rtap = (int)tap_off;
+            tap_off += (long long)og.rtap_stride * g.L;
+        }
         og.grp_begin = grp;
         make_magic((unsigned)std::max(1, og.gpr), &og.gpr_magic, &og.gpr_shift);
         grp += (long long)og.rows * og.gpr;
