@@ -200,7 +200,9 @@ enum {
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (default, S <= 3), 1 LDS tiles */
     GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian sweep: output rows per wave strip (16 default, 32) */
     GDP_TUNE_CONV_ORDER = 11    /* gdp_build_gaussian sweep: bit 0 XCD-chunked block order, bit 1 odd waves
-                                   sweep bottom-up (shared halo rows loaded together); default 0 */
+                                   sweep bottom-up (shared halo rows loaded together), bit 2 octave
+                                   o's block rows issued right after the octave-0 rows covering
+                                   their input rows; default 5 (bits 0 + 2) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

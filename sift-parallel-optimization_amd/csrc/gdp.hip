@@ -85,9 +85,12 @@ struct gdp_ctx {
     float* d_taps = nullptr;
     int conv_kernel = 0;          // GDP_TUNE_CONV_KERNEL: 0 register sweep (default), 1 LDS tiles
     int conv_rows = 16;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep
-    int conv_order = 0;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions
+    int conv_order = 5;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
+                                  // bit 2 input-row-interleaved octaves (conv_sweep_perm)
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
     int* d_cradius = nullptr;     // convolution-mode radius per scale
+    unsigned* d_conv_perm = nullptr; // conv sweep block order for GDP_TUNE_CONV_ORDER bit 2 (per image)
+    bool conv_perm_dirty = true;
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
     float* h_stage = nullptr;     // pinned staging for row-pointer downloads (largest level)
     size_t h_stage_floats = 0;
@@ -244,13 +247,56 @@ static void conv_sweep_geom(gdp_ctx* c) {
         g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
         g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
     }
+    c->conv_perm_dirty = true;
+}
+
+// Input-row-interleaved block order of the convolution sweep (GDP_TUNE_CONV_ORDER bit 2): each
+// octave-o block row (kSwWaves * conv_rows output rows = 2^o times as many input rows) is issued
+// right after the octave-0 block row that covers the last of its input rows, so the decimated
+// rows it reads were just brought on chip by octave 0 instead of being fetched again.
+static int conv_sweep_perm(gdp_ctx* c) {
+    const Geom& g = c->geom;
+    std::vector<unsigned> perm;
+    perm.reserve(g.sw_blk[g.O]);
+    auto emit_row = [&](int o, unsigned tr) {
+        const unsigned sc = (unsigned)g.sw_strips_c[o];
+        for (unsigned tc = 0; tc < sc; ++tc) perm.push_back(g.sw_blk[o] + tr * sc + tc);
+    };
+    const unsigned rows0 = g.oct[0].cols ? (g.sw_blk[1] - g.sw_blk[0]) / std::max(1u, (unsigned)g.sw_strips_c[0]) : 0;
+    std::vector<unsigned> next(g.O, 0); // next block row of each octave
+    for (unsigned k = 0; k < rows0; ++k) {
+        emit_row(0, k);
+        for (int o = 1; o < g.O; ++o) {
+            const unsigned sc = (unsigned)std::max(1, g.sw_strips_c[o]);
+            const unsigned nrows = (g.sw_blk[o + 1] - g.sw_blk[o]) / sc;
+            // octave-o block row tr covers octave-0 block rows [2^o tr, 2^o (tr + 1))
+            while (next[o] < nrows && ((unsigned long long)(next[o] + 1) << o) <= (unsigned long long)k + 1)
+                emit_row(o, next[o]++);
+        }
+    }
+    for (int o = 0; o < g.O; ++o) { // leftovers (octave 0 swept nothing, or rounding at the bottom)
+        const unsigned sc = (unsigned)std::max(1, g.sw_strips_c[o]);
+        const unsigned nrows = (g.sw_blk[o + 1] - g.sw_blk[o]) / sc;
+        if (o == 0) continue;
+        while (next[o] < nrows) emit_row(o, next[o]++);
+    }
+    if (perm.size() != g.sw_blk[g.O]) return c->status(GDP_ERR_STATE, "conv sweep order: %zu of %u blocks", perm.size(), g.sw_blk[g.O]);
+    if (c->d_conv_perm) GDP_HIP(c, hipFree(c->d_conv_perm));
+    c->d_conv_perm = nullptr;
+    if (!perm.empty()) {
+        GDP_HIP(c, hipMalloc(&c->d_conv_perm, perm.size() * sizeof(unsigned)));
+        GDP_HIP(c, hipMemcpy(c->d_conv_perm, perm.data(), perm.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    }
+    c->conv_perm_dirty = false;
+    return GDP_OK;
 }
 
 template <int L, int T>
 hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     auto k = k_conv_sweep<L, T, kSwV>;
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kSwWaves), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kSwWaves), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
+                       c->d_conv_perm);
     return hipGetLastError();
 }
 
@@ -443,6 +489,7 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_out_own) (void)hipFree(c->d_out_own);
     if (c->d_ctaps) (void)hipFree(c->d_ctaps);
     if (c->d_cradius) (void)hipFree(c->d_cradius);
+    if (c->d_conv_perm) (void)hipFree(c->d_conv_perm);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->d_sum) (void)hipFree(c->d_sum);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -609,6 +656,10 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) {
     // the register sweep is compiled for S = 0..3 (L = 3..6) and takes the octaves whose width is a
     // multiple of 4; the LDS tiles take the rest (and everything for other S or conv_kernel = 1)
     const bool sweep = c->conv_kernel == 0 && g.L >= 3 && g.L <= 6;
+    if (sweep && (c->conv_order & 4) && c->conv_perm_dirty) {
+        const int rc = conv_sweep_perm(c);
+        if (rc != GDP_OK) return rc;
+    }
     if (sweep) {
         const long long grid = (long long)g.sw_blk[g.O] * g.batch;
         if (grid >= (1ll << 31) - 8) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
@@ -948,7 +999,7 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
             return rc;
         }
         case GDP_TUNE_CONV_ORDER:
-            if (value < 0 || value > 3) return c->status(GDP_ERR_ARG, "conv order must be 0..3");
+            if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;
             return GDP_OK;
         case GDP_TUNE_TILE_ORDER:

@@ -620,11 +620,13 @@ _CONV_SHAPES = [(64, 96, 2, 0, "i32", 1), (300, 500, 3, 5, "i32", 1), (1080, 192
                 (17, 33, 1, 0, "i32", 1), (70, 240, 0, 0, "i32", 2), (129, 484, 2, 4, "i32", 1), (40, 50, 5, 0, "i32", 1)]
 _CONV_KERNELS = [dict(conv_kernel=0, conv_rows=16, conv_order=0), dict(conv_kernel=0, conv_rows=32, conv_order=0),
                  dict(conv_kernel=0, conv_rows=16, conv_order=3), dict(conv_kernel=0, conv_rows=32, conv_order=2),
+                 dict(conv_kernel=0, conv_rows=16, conv_order=4), dict(conv_kernel=0, conv_rows=32, conv_order=5),
                  dict(conv_kernel=1)]
 
 
 @pytest.mark.parametrize("H,W,S,O,fmt,batch", _CONV_SHAPES)
-@pytest.mark.parametrize("tune", _CONV_KERNELS, ids=["sweep16", "sweep32", "sweep16xcd_alt", "sweep32alt", "tiles"])
+@pytest.mark.parametrize("tune", _CONV_KERNELS, ids=["sweep16", "sweep32", "sweep16xcd_alt", "sweep32alt",
+                                                          "sweep16rowmix", "sweep32rowmix_xcd", "tiles"])
 def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt, batch, tune):
     """Extension mode (no reference counterpart; parity unpinned by construction): checked against
     a float64 separable convolution, for both kernels (register sweep with DPP lane shifts, LDS
