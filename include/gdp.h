@@ -107,7 +107,9 @@ int gdp_set_input_host_u8(gdp_ctx* ctx, int b, const uint8_t* base, size_t pitch
 int gdp_set_input_device_u8(gdp_ctx* ctx, const uint8_t* base, size_t pitch, size_t image_stride);
 /* Benchmark/test input generated on the device (SURVEY.md §8d counter hash): image b of the
  * batch gets global index first_image + b; pixel = lowbias32(seed ^ fold(idx)) >> 24 with
- * idx = (index*H + r)*W + c over the WHOLE image (band contexts generate their rows only). */
+ * idx = (index*H + r)*W + c over the WHOLE image (band contexts generate their rows only).
+ * Writes the input the builds read: the context's own buffer, or the caller's device buffer
+ * bound by gdp_set_input_device* (its pitch and image stride; the pitch padding is untouched). */
 int gdp_fill_synthetic(gdp_ctx* ctx, uint32_t seed, long first_image, void* stream);
 
 /* ---- compute ------------------------------------------------------------------------------- */
@@ -199,10 +201,12 @@ enum {
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (default, S <= 3), 1 LDS tiles */
     GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian sweep: output rows per wave strip (16 default, 32) */
-    GDP_TUNE_CONV_ORDER = 11    /* gdp_build_gaussian sweep: bit 0 XCD-chunked block order, bit 1 odd waves
+    GDP_TUNE_CONV_ORDER = 11,   /* gdp_build_gaussian sweep: bit 0 XCD-chunked block order, bit 1 odd waves
                                    sweep bottom-up (shared halo rows loaded together), bit 2 octave
                                    o's block rows issued right after the octave-0 rows covering
                                    their input rows; default 5 (bits 0 + 2) */
+    GDP_TUNE_BUILD_LDS = 12     /* gdp_build: dynamic LDS bytes requested per block (0 default);
+                                   used only to cap resident blocks per CU (occupancy) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

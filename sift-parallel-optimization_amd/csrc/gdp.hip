@@ -87,6 +87,7 @@ struct gdp_ctx {
     int conv_rows = 16;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep
     int conv_order = 5;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
                                   // bit 2 input-row-interleaved octaves (conv_sweep_perm)
+    int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
     int* d_cradius = nullptr;     // convolution-mode radius per scale
     unsigned* d_conv_perm = nullptr; // conv sweep block order for GDP_TUNE_CONV_ORDER bit 2 (per image)
@@ -173,8 +174,8 @@ int launch_build(gdp_ctx* c, hipStream_t st) {
     const long long cap = c->grid_override > 0 ? c->grid_override : (c->persistent ? c->blocks_max : units);
     const int grid = (int)std::min<long long>(units, cap);
     const BuildVariant& v = kVariants[c->variant];
-    hipLaunchKernelGGL(v.k[g.L == 5][c->nontemporal ? 1 : 0], dim3(grid), dim3(v.block), 0, st, c->d_geom, c->d_in,
-                       c->d_out, c->d_taps);
+    hipLaunchKernelGGL(v.k[g.L == 5][c->nontemporal ? 1 : 0], dim3(grid), dim3(v.block), (unsigned)c->build_lds, st,
+                       c->d_geom, c->d_in, c->d_out, c->d_taps);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
 }
@@ -612,12 +613,13 @@ int gdp_get_input_format(const gdp_ctx* c) { return c ? c->geom.in_fmt : -1; }
 
 int gdp_fill_synthetic(gdp_ctx* c, uint32_t seed, long first_image, void* stream) {
     if (!c) return GDP_ERR_ARG;
-    if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
     GDP_HIP(c, hipSetDevice(c->device));
     const long long total = (long long)c->geom.in_rows * c->geom.W * c->geom.batch;
     const int grid = (int)std::min<long long>((total + kBlock - 1) / kBlock, c->blocks_max);
-    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(kBlock), 0, c->pick(stream), c->d_geom, c->d_in_own, seed,
-                       (long long)first_image);
+    // the images land in whatever input the builds read: the context's own buffer, or the caller's
+    // device buffer bound by gdp_set_input_device* (its pitch / image stride)
+    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(kBlock), 0, c->pick(stream), c->d_geom, const_cast<void*>(c->d_in),
+                       seed, (long long)first_image);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
 }
@@ -957,6 +959,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_CONV_KERNEL: *value = c->conv_kernel; return GDP_OK;
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
+        case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 }
@@ -1001,6 +1004,10 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
         case GDP_TUNE_CONV_ORDER:
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;
+            return GDP_OK;
+        case GDP_TUNE_BUILD_LDS:
+            if (value < 0 || value > 160 * 1024) return c->status(GDP_ERR_ARG, "build LDS bytes must be in [0, 163840]");
+            c->build_lds = value;
             return GDP_OK;
         case GDP_TUNE_TILE_ORDER:
             if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");

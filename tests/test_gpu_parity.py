@@ -122,7 +122,7 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
         with pkg.PyramidContext(H, W, S=S, octaves=O) as ctx:
             ctx.set_input(img)
             for kw in ({"variant": variant}, {"tile_order": 1}, {"tile_order": 2}, {"nontemporal": 0},
-                       {"blocks_per_cu": 1}, {"grid": 3}):
+                       {"blocks_per_cu": 1}, {"grid": 3}, {"blocks_per_cu": 0, "grid": 0, "build_lds": 41984}):
                 ctx.set_tuning(**kw)
                 ctx.build()
                 _assert_same(ctx.pyramid(0), want, (variant, H, W, S, O, kw))
@@ -131,7 +131,7 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
 def test_default_variant_follows_geometry(pkg):
     with pkg.PyramidContext(64, 4096, S=2, batch=2) as a, pkg.PyramidContext(64, 1920, S=2) as b, \
             pkg.PyramidContext(4096, 4096, S=2, octaves=5) as c:
-        assert a.tuning()["variant"] == 0 and b.tuning()["variant"] == 11 and c.tuning()["variant"] == 9
+        assert a.tuning()["variant"] == 0 and b.tuning()["variant"] == 11 and c.tuning()["variant"] == 0
 
 
 def test_autotune_keeps_results_bit_exact(pkg, oracle):
@@ -211,6 +211,28 @@ def test_device_input_binding(pkg, oracle):
             torch.cuda.synchronize()
             for b in range(2):
                 _assert_same(ctx.pyramid(b), oracle.build_pyramid(imgs[b], 2), ("devin", H, W, pitch, b))
+            ctx.unbind_device_input()
+
+
+def test_synthetic_fill_into_bound_device_input(pkg, oracle):
+    """gdp_fill_synthetic writes the input the builds read: a caller's pitched device buffer
+    (int32 and uint8) gets the generator's images and its pitch padding is left alone."""
+    import torch
+
+    H, W, B, first = 50, 37, 2, 5
+    for fmt, dt, pitch in [("i32", torch.int32, 41), ("u8", torch.uint8, 64)]:
+        dev = torch.full((B, H, pitch), 7, dtype=dt, device="cuda")
+        with pkg.PyramidContext(H, W, S=2, batch=B, input_format=fmt) as ctx:
+            ctx.bind_device_input(dev.data_ptr(), pitch, H * pitch, keepalive=dev)
+            ctx.fill_synthetic(0x5EED, first, torch.cuda.current_stream())
+            ctx.build(torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            host = dev.cpu().numpy().astype(np.int64)
+            assert (host[:, :, W:] == 7).all(), fmt
+            for b in range(B):
+                img = oracle.synthetic_image(H, W, 0x5EED, first + b)
+                np.testing.assert_array_equal(host[b, :, :W], img)
+                _assert_same(ctx.pyramid(b), oracle.build_pyramid(img, 2), ("synth bound", fmt, b))
             ctx.unbind_device_input()
 
 

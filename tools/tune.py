@@ -30,15 +30,19 @@ def main():
     ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
     ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="buffer sets the timed launches cycle through (bench.py's cold-cache steps)")
     args = ap.parse_args()
     pkg = entry.load_package()
     cfg = bench.CONFIGS[args.config]
     H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
     if args.shape:
         H, W, B = (int(x) for x in args.shape.split("x"))
-    ctx = pkg.PyramidContext(H, W, S=2, octaves=O, batch=B)
-    ctx.fill_synthetic(bench.SEED, 0)
-    ctx.sync()
+    ctxs = [pkg.PyramidContext(H, W, S=2, octaves=O, batch=B) for _ in range(args.rotate)]
+    for c in ctxs:
+        c.fill_synthetic(bench.SEED, 0)
+        c.sync()
+    ctx = ctxs[0]
     ref = None
     variants = []
     for v in args.variants.split(";"):
@@ -47,7 +51,7 @@ def main():
                              "variant": int(kv.get("v", -1)) if "v" in kv else None,
                              "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1)),
                              "conv_kernel": int(kv.get("ck", 0)), "conv_rows": int(kv.get("cr", 16)),
-                             "conv_order": int(kv.get("co", 0))}))
+                             "conv_order": int(kv.get("co", 0)), "build_lds": int(kv.get("lds", 0))}))
         if variants[-1][1]["variant"] is None:
             del variants[-1][1]["variant"]
         if "bpc" in kv:
@@ -55,11 +59,9 @@ def main():
     times = {name: [] for name, _ in variants}
 
     def apply(kw):  # fresh context state per variant: persistent only when bpc is given
-        ctx.set_tuning(**{k: v for k, v in kw.items() if k != "blocks_per_cu"})
-        if "blocks_per_cu" in kw:
-            ctx.set_tuning(blocks_per_cu=kw["blocks_per_cu"])
-        else:
-            ctx.set_tuning(blocks_per_cu=0)
+        for c in ctxs:
+            c.set_tuning(**{k: v for k, v in kw.items() if k != "blocks_per_cu"})
+            c.set_tuning(blocks_per_cu=kw.get("blocks_per_cu", 0))
 
     for name, kw in variants:  # warm-up + identical-output check for every variant
         apply(kw)
@@ -77,18 +79,23 @@ def main():
     import torch
 
     stream = torch.cuda.Stream()
-    step = {"build": ctx.build, "regen": ctx.generate_dog, "gauss": lambda st: ctx.gauss_range(0, O, st),
-            "conv": ctx.build_gaussian}[args.op]
+    steps = [{"build": c.build, "regen": c.generate_dog, "gauss": lambda st, c=c: c.gauss_range(0, O, st),
+              "conv": c.build_gaussian}[args.op] for c in ctxs]
+    if args.op in ("regen", "gauss"):
+        for c in ctxs:
+            c.build(stream)
     for _ in range(args.rounds):
         for name, kw in variants:
             apply(kw)
-            if args.op == "build":
+            if args.op == "build" and args.rotate == 1:
                 times[name].append(ctx.time_builds(args.iters) / args.iters)
             else:
+                for st in steps:
+                    st(stream)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                for _ in range(args.iters):
-                    step(stream)
+                for i in range(args.iters):
+                    steps[i % len(steps)](stream)
                 e1.record(stream)
                 e1.synchronize()
                 times[name].append(e0.elapsed_time(e1) / args.iters)
@@ -101,7 +108,8 @@ def main():
         print(json.dumps({"variant": name, "config": args.config, "shape": [H, W, B], "ms_median": round(float(np.median(t)), 5),
                           "ms_min": round(float(t.min()), 5),
                           "GBps_median": round(nbytes / (np.median(t) / 1e3) / 1e9, 1)}), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
 
 
 if __name__ == "__main__":
