@@ -1048,4 +1048,11 @@ int gdp_time_builds(gdp_ctx* c, int iters, void* stream, float* total_ms) {
     return rc;
 }
 
+#ifdef GDP_TRACE_BLOCKS
+// Diagnostic build only: device buffer of 3 x u64 per block for the next build launches (NULL off).
+int gdp_debug_set_block_trace(void* dev_buf) {
+    unsigned long long* p = static_cast<unsigned long long*>(dev_buf);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_block_trace), &p, sizeof p) == hipSuccess ? GDP_OK : GDP_ERR_HIP;
+}
+#endif
 }  // extern "C"

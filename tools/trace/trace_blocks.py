@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Ramp and tail of one cold k_build launch, from per-block timestamps (diagnostic build).
+
+    make -C tools/trace && python tools/trace/trace_blocks.py [--shape 4096x4096x1] [--variant 0]
+
+Builds tools/trace/libgdp_trace.so's k_build over `--rotate` buffer sets (so the traced launch is
+cold, as in bench.py), then traces one launch: per WAVE the 100 MHz real-time clock at entry and
+after its last store was issued, and its XCC.  Prints one JSON line per repeat: launch span, when
+the last wave STARTED, the spread of wave end times, mean wave lifetime per dispatch round,
+per-XCC first-start / last-end.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+os.environ.setdefault("GDP_LIBRARY", os.path.join(HERE, "libgdp_trace.so"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="4096x4096x1")
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--order", type=int, default=0)
+    ap.add_argument("--rotate", type=int, default=5)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    from importlib import import_module
+
+    lib = import_module(pkg.__name__ + "._lib").lib()
+    lib.gdp_debug_set_block_trace.argtypes = [ctypes.c_void_p]
+    H, W, B = (int(x) for x in args.shape.split("x"))
+    ctxs = [pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) for _ in range(args.rotate)]
+    for c in ctxs:
+        c.fill_synthetic(0x5EED, 0)
+        c.set_tuning(variant=args.variant, tile_order=args.order)
+    for _ in range(3):
+        for c in ctxs:
+            c.build()
+    for c in ctxs:
+        c.sync()
+    blocks = 1 << 24  # wave records
+    buf = torch.zeros(3 * blocks, dtype=torch.int64, device="cuda")
+    out = []
+    for rep in range(3):
+        for c in ctxs[1:]:
+            c.build()
+        for c in ctxs:
+            c.sync()
+        buf.zero_()
+        torch.cuda.synchronize()
+        assert lib.gdp_debug_set_block_trace(ctypes.c_void_p(buf.data_ptr())) == 0
+        ctxs[0].build()
+        ctxs[0].sync()
+        assert lib.gdp_debug_set_block_trace(None) == 0
+        t = buf.cpu().numpy().reshape(-1, 3)
+        t = t[t[:, 0] != 0]
+        t0 = t[:, 0].min()
+        start = (t[:, 0] - t0) / 100.0  # us
+        end = (t[:, 1] - t0) / 100.0
+        xcc = (t[:, 2] >> 32) & 0xF
+        life = end - start
+        order = np.argsort(start)
+        n = len(t)
+        span = float(end.max())
+        # dispatch rounds: blocks sorted by start, cut into groups of the resident count
+        resident = int((start < float(end.min())).sum())  # waves started before the first one ended
+        rounds = [float(life[order[i:i + resident]].mean()) for i in range(0, n, max(resident, 1))]
+        rec = {"rep": rep, "waves": n, "span_us": round(span, 2), "last_block_start_us": round(float(start.max()), 2),
+               "first_block_end_us": round(float(end.min()), 2),
+               "end_p10_p50_p90_us": [round(float(np.percentile(end, p)), 2) for p in (10, 50, 90)],
+               "lifetime_mean_us": round(float(life.mean()), 2), "resident_at_start": resident,
+               "lifetime_by_round_us": [round(x, 2) for x in rounds[:12]],
+               "idle_tail_us": round(span - float(np.percentile(end, 50)), 2),
+               "xcc_first_start_last_end_us": {int(x): [round(float(start[xcc == x].min()), 2),
+                                                        round(float(end[xcc == x].max()), 2)] for x in np.unique(xcc)}}
+        # fraction of the span with fewer than half the resident blocks running
+        grid = np.linspace(0, span, 400)
+        running = np.array([((start <= g) & (end > g)).sum() for g in grid])
+        rec["us_below_half_resident"] = round(float((running < resident / 2).mean() * span), 2)
+        out.append(rec)
+        print(json.dumps(rec), flush=True)
+    for c in ctxs:
+        c.close()
+
+
+if __name__ == "__main__":
+    main()
