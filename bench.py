@@ -186,6 +186,46 @@ def autotune_rotating(ctxs, stream, iters, rounds=5):
     return best[0], best[1], med[best]
 
 
+def scatter_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
+    """SURVEY.md §8e's optional image-batch split, measured OUTSIDE the timed region: rank 0
+    generates every rank's images (the same global indices the ranks otherwise generate locally),
+    one collective scatter (RCCL over xGMI; gloo + host staging in rehearsals) hands each rank
+    its share, and every rank builds from the scattered images and checks that each image's
+    pyramid checksum equals the one built from its locally generated copy."""
+    import torch
+
+    H, W, B = cfg["H"], cfg["W"], cfg["batch"]
+    dt = torch.uint8 if in_fmt == "u8" else torch.int32
+    dev = torch.device("cuda", torch.cuda.current_device())
+    per = B * H * W
+
+    def fill(chunk, r):  # the device generator writes straight into rank r's share
+        stage = chunk if chunk.is_cuda else torch.empty(per, dtype=dt, device=dev)
+        ctx.bind_device_input(stage.data_ptr(), W, H * W, keepalive=stage)
+        ctx.fill_synthetic(SEED, r * B)
+        ctx.sync()
+        ctx.unbind_device_input()
+        if stage is not chunk:
+            chunk.copy_(stage.cpu())
+
+    recv, secs = mg.scatter_images(per, fill, dist=dist, device=dev if backend == "nccl" else "cpu", dtype=dt)
+    recv = recv.to(dev)
+    ctx.build()
+    ctx.sync()
+    local = [ctx.checksum(b) for b in range(B)]
+    ctx.bind_device_input(recv.data_ptr(), W, H * W, keepalive=recv)
+    ctx.build()
+    ctx.sync()
+    got = [ctx.checksum(b) for b in range(B)]
+    ctx.unbind_device_input()
+    secs, bad = mg.max_over_ranks([secs, float(local != got)], dist=dist,
+                                  device="cuda" if backend == "nccl" else "cpu")
+    nbytes = world * per * (1 if in_fmt == "u8" else 4)
+    return {"mode": f"collective scatter of rank 0's batch ({'RCCL over xGMI' if backend == 'nccl' else backend + ' via host'}), "
+                    "outside the timed region", "bytes": nbytes, "ms": round(secs * 1e3, 3),
+            "GBps": round(nbytes / secs / 1e9, 1) if secs > 0 else None, "bit_exact": bad == 0.0}
+
+
 def verify(ctx, cfg, key, world, rank, dist, mg):
     """After the timed region: gdp_checksum of what the benchmark built vs the checksum of the
     reference's own output for the same input (tests/golden/checksums.json).  Image configs check
@@ -247,6 +287,9 @@ def main():
     ap.add_argument("--conv-kernel", type=int, default=None, help="--op conv: 0 register sweep, 1 LDS tiles")
     ap.add_argument("--conv-rows", type=int, default=None, help="--op conv sweep: rows per wave strip (16/32)")
     ap.add_argument("--conv-order", type=int, default=None, help="--op conv sweep: bit 0 XCD-chunked, bit 1 alternate directions")
+    ap.add_argument("--scatter", action="store_true",
+                    help="N > 1, image configs: also measure the image-batch split (rank 0's batch scattered over "
+                         "RCCL, SURVEY.md §8e), outside the timed region, and check the ranks build the same bits from it")
     ap.add_argument("--rotate", type=int, default=None,
                     help="independent input+pyramid buffer sets the steps cycle through (default: enough to "
                          "exceed %d MiB, so no step finds its lines in the 256 MB Infinity Cache)" % (ROTATE_BYTES >> 20))
@@ -311,6 +354,9 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
 
+    distribution = None
+    if args.scatter and world > 1 and not cfg["band"]:
+        distribution = scatter_split(ctx, cfg, world, rank, dist, mg, backend, args.input)
     for c in ctxs:
         c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order)
     autotuned = None
@@ -419,6 +465,8 @@ def main():
         },
     }
     result["parity"] = parity if args.op == "build" else {"status": "not checked for in-place re-entry ops"}
+    if distribution is not None:
+        result["distribution"] = distribution
     if args.op != "build":
         result["metric"] = METRIC + (" [op=conv: true-Gaussian extension, not the reference's algorithm]"
                                      if args.op == "conv" else f" [op={args.op}: in-place pass]")

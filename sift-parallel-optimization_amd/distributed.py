@@ -90,6 +90,41 @@ def gather_checksums(local, dist=None, dst=0):
     return out
 
 
+def scatter_images(per_rank, fill, dist=None, device="cpu", dtype=None):
+    """The image-batch split of SURVEY.md §8e's optional path: rank 0 holds every rank's images
+    (`fill(chunk, r)` writes rank r's `per_rank` elements into `chunk`) and one collective scatter
+    (RCCL over xGMI on GPUs, gloo on CPU) hands each rank its share.  Returns (this rank's
+    elements, seconds of the scatter between two barriers)."""
+    import time
+
+    import torch
+
+    dtype = dtype or torch.int32
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    recv = torch.empty(per_rank, dtype=dtype, device=device)
+    chunks = None
+    if rank == 0:
+        big = torch.empty(world * per_rank, dtype=dtype, device=device)
+        chunks = [big[r * per_rank:(r + 1) * per_rank] for r in range(world)]
+        for r, ch in enumerate(chunks):
+            fill(ch, r)
+    sync = torch.cuda.synchronize if torch.device(device).type == "cuda" else (lambda: None)
+    sync()
+    if world == 1:
+        t0 = time.perf_counter()
+        recv.copy_(chunks[0])
+        sync()
+        return recv, time.perf_counter() - t0
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    dist.scatter(recv, chunks, src=0)
+    sync()
+    dist.barrier()
+    return recv, time.perf_counter() - t0
+
+
 def assemble_bands(H, W, S, octaves, world, packed_bands, like=None):
     """Collector-side assembly: the packed band pyramids of ranks 0..world-1 (torch tensors,
     any device) -> the packed pyramid of the whole image, in the oracle's [o][s][rows][cols]

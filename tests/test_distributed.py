@@ -107,6 +107,46 @@ def test_collector_generate_dog_mgpu_over_gloo(pkg, n, S, O, world):
     assert root[0][3] == [[r * 10 + 1, r * 10 + 2] for r in range(world)]
 
 
+def _scatter_worker(rank, world, port, per, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, REPO)
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    d = __import__(pkg.__name__ + ".distributed", fromlist=["x"])
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        # rank 0 fills rank r's share with the synthetic images' generator stand-in r*1000 + i
+        fill = lambda ch, r: ch.copy_(torch.arange(per, dtype=torch.int32) + r * 1000)
+        got, secs = d.scatter_images(per, fill, dist=dist)
+        ok = bool(torch.equal(got, torch.arange(per, dtype=torch.int32) + rank * 1000))
+        t = d.max_over_ranks([secs], dist=dist)
+        q.put((rank, ok, t[0] >= 0.0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,per", [(2, 4096), (3, 1000)])
+def test_scatter_images_over_gloo(pkg, world, per):
+    """The image-batch split (bench.py's scatter of rank 0's batch, RCCL on GPUs) on gloo ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, per, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[0] for r in results] == list(range(world))
+    assert all(r[1] and r[2] for r in results), results
+
+
 def test_checksum_restatement_is_order_independent(oracle):
     """Band checksums add up to the whole image's (the property gdp_checksum relies on)."""
     n, S, O = 64, 2, 5
