@@ -110,6 +110,16 @@ def cpu_baseline(budget_s):
             out["serial_full_semantics"] = {"value": round(n * n / (serial["ms_median"] / 1e3) / 1e6, 3),
                                             "unit": "Mpix/s", "cores": 1,
                                             "sample": f"GuassDePyramid.h GenerateDoG, {n}x{n}, median of {serial['reps']}"}
+        # the reference's fastest FULL-semantics CPU path: AVX-512 x pthreads, octaves round-robin
+        # over its own 7 worker threads (GaussDePyramid-AVX512xPTHREAD.h:143-261)
+        xp_probe = oracle.ref_time("time-a512xp", n, S, spec, 2)
+        if xp_probe:
+            xp_reps = max(3, min(200, int(0.3 * budget_s / max(xp_probe["ms_median"] / 1e3, 1e-4))))
+            xp = oracle.ref_time("time-a512xp", n, S, spec, xp_reps)
+            out["a512xp_full_semantics"] = {
+                "value": round(n * n / (xp["ms_median"] / 1e3) / 1e6, 3), "unit": "Mpix/s", "cores": 7,
+                "sample": f"GaussPyramid_a512xp::GenerateDoG (reference header compiled in place, 7 pthreads), "
+                          f"{n}x{n}, all {xp.get('octaves', '?')} octaves, median of {xp['reps']} calls; GaussPyInit untimed"}
         return out
     import numpy as np
 
