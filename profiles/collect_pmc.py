@@ -82,6 +82,20 @@ def main():
             for line in f:
                 if line.startswith("{"):
                     rec["bench_line_of_traced_run"] = json.loads(line)
+    # the timed region alone: the last `steps` dispatches of the kernel in the trace (the stats
+    # row also averages the autotuning and warm-up launches)
+    trace_csv = os.path.join(args.trace, "run_kernel_trace.csv")
+    line = rec.get("bench_line_of_traced_run")
+    if line and os.path.exists(trace_csv):
+        with open(trace_csv) as f:
+            durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                    for r in sorted((r for r in csv.DictReader(f) if r["Kernel_Name"] == name),
+                                    key=lambda r: int(r["Start_Timestamp"]))]
+        timed = durs[-int(line["steps"]):]
+        if timed:
+            rec["trace_timed_steps"] = len(timed)
+            rec["trace_timed_avg_ns"] = statistics.mean(timed)
+            rec["bench_kernel_ms"] = line["roofline"]["kernel_ms"]
     tag = args.config if args.op == "build" else f"{args.config}_{args.op}"
     rec["op"] = args.op
     out = os.path.join(HERE, f"pmc_{tag}_{args.round}.json")
