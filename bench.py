@@ -160,9 +160,10 @@ def latest_pmc(config_key):
 
 def autotune_rotating(ctxs, stream, iters, rounds=5):
     """gdp_autotune's search (every build variant x tile order 0/1) over the ROTATED step sequence
-    the benchmark times, so the pick is made on cold (not MALL-resident) buffers; candidates are
-    interleaved round-robin over `rounds` rounds and ranked by their median (drift hits all
-    alike).  All candidates give identical bits."""
+    the benchmark times (one set when it alone exceeds the MALL), so the pick is made on cold
+    buffers; candidates are interleaved round-robin over `rounds` rounds and ranked by their
+    median (drift hits all alike, unlike gdp_autotune's one-candidate-at-a-time timing).  All
+    candidates give identical bits."""
     import torch
 
     import __graft_entry__ as entry
@@ -374,9 +375,8 @@ def main():
         for c in ctxs:
             c.set_tuning(variant=args.variant)
     elif args.op == "build" and not args.no_autotune:
-        iters = 3 if B * H * W > (1 << 28) else 10
-        autotuned = (ctx.autotune(iters=iters, stream=stream) if rotate == 1
-                     else autotune_rotating(ctxs, stream, iters))
+        # candidates interleaved round-robin (drift hits all alike), over the rotated sets
+        autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10)
     if args.op == "build":
         steps_fn = [c.build for c in ctxs]
     elif args.op == "conv":
