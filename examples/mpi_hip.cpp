@@ -31,7 +31,7 @@ int main(int argc, char* argv[]) {
     }
     GaussPyramid_hip_mpi g(p, n, 2);
     if (argc > 3) {  // parity mode: one collective build, the collector dumps its GaussPy
-        g.GenerateDoG_mpi(argc, argv);
+        g.GenerateDoG_mgpu(argc, argv);  // = GenerateDoG_mpi (the SURVEY's name for the RCCL form)
         if (g.rank() == 0) {
             FILE* f = std::fopen(argv[3], "wb");
             for (int o = 0, len = n; len; ++o, len /= 2)

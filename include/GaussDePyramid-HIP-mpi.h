@@ -44,6 +44,9 @@ public:
     void GenerateDoG();
     void GenerateDoG_mpi_normal() {}  // empty in the reference (:337-339)
     void GenerateDoG_mpi(int argc, char** argv);
+    // SURVEY.md §8(b)/(f2)'s name for the same entry point: the RCCL counterpart of
+    // GenerateDoG_mpi (GaussDePyramid-MPI.h:265), same signature and collector semantics.
+    void GenerateDoG_mgpu(int argc, char** argv) { GenerateDoG_mpi(argc, argv); }
     ~GaussPyramid_hip_mpi();
     int thread_count;  // kept for source compatibility (:39-43); unused on the GPU
     int chunk_size;

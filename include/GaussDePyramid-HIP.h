@@ -46,6 +46,7 @@ public:
     // does the whole pyramid, so the result every caller sees is the collector's.  Unlike the
     // reference (MPI_Init/MPI_Finalize inside) it may be called any number of times.
     void GenerateDoG_mpi(int argc, char** argv);
+    void GenerateDoG_mgpu(int argc, char** argv) { GenerateDoG_mpi(argc, argv); }  // SURVEY §8(f2) name
     ~GaussPyramid_hip();
     bool initialized;
     bool mirror_host;  // copy the pyramid into GaussPy after every mutating call (default true)
