@@ -192,7 +192,7 @@ enum {
     GDP_TUNE_BLOCKS_PER_CU = 2, /* value > 0: persistent build grid = CUs x value;
                                    0 (default): one 16x256 tile per block                      */
     GDP_TUNE_GRID = 3,          /* explicit build grid size; 0 (default) = automatic         */
-    GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile shape), 0..14;
+    GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile shape), 0..18;
                                    default chosen from the image width                         */
     GDP_TUNE_TILE_ORDER = 5,    /* build tile order: 0 linear (default), 1 XCD-chunked,
                                    2 XCD row-interleaved                                       */

@@ -431,10 +431,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     }
     g.tail_groups_per_img = (unsigned)tail_per_img;
     g.tail_units = (unsigned)tail_units;
-    // Tile order default (tools/tune.py, MI355X): a single very large image (>= 64 Mpix, e.g. the
-    // 16384^2 config) streams 7-8 % faster when each XCD sweeps its own contiguous eighth of the
-    // tiles; batches and <= 4096^2 images are fastest in linear order.
-    g.tile_order = (batch == 1 && (long long)g.in_rows * W >= (1ll << 26)) ? 1 : 0;
+    // Tile order default: linear.  (With v0 a single >= 64 Mpix image streamed 7-8 % faster in
+    // the XCD-chunked order; with the default v15 the linear order is the faster one on 16384^2,
+    // 1.344 vs 1.375 ms, and batches differ box to box — gdp_autotune measures both.)
+    g.tile_order = 0;
     retile(c, kVariants[c->variant].tile_cols, kVariants[c->variant].tile_rows);
     conv_sweep_geom(c);
     c->h_taps.assign((size_t)tap_off, 0.0f);

@@ -87,6 +87,15 @@ def main():
         grid = np.linspace(0, span, 400)
         running = np.array([((start <= g) & (end > g)).sum() for g in grid])
         rec["us_below_half_resident"] = round(float((running < resident / 2).mean() * span), 2)
+        rec["max_running_waves"] = int(running.max())
+        rec["running_p50_over_span"] = int(np.median(running))
+        # per CU (XCC, SE, SA?, CU from HW_ID) peak concurrency at the busiest sampled instant
+        hw = t[:, 2] & 0xFFFFFFFF
+        cu = (xcc << 16) | ((hw >> 13) & 0x7) << 8 | ((hw >> 12) & 0x1) << 4 | ((hw >> 8) & 0xF)
+        g = grid[int(np.argmax(running))]
+        live = (start <= g) & (end > g)
+        _, per_cu = np.unique(cu[live], return_counts=True)
+        rec["waves_per_cu_at_peak"] = [int(per_cu.min()), int(np.median(per_cu)), int(per_cu.max()), int(len(per_cu))]
         out.append(rec)
         print(json.dumps(rec), flush=True)
     for c in ctxs:
