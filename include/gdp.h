@@ -204,7 +204,8 @@ enum {
     GDP_TUNE_CONV_ORDER = 11,   /* gdp_build_gaussian sweep: bit 0 XCD-chunked block order, bit 1 odd waves
                                    sweep bottom-up (shared halo rows loaded together), bit 2 octave
                                    o's block rows issued right after the octave-0 rows covering
-                                   their input rows; default 5 (bits 0 + 2) */
+                                   their input rows; default 5 for batches, 4 for one
+                                   image >= 64 Mpix, 0 for smaller single images */
     GDP_TUNE_BUILD_LDS = 12     /* gdp_build: dynamic LDS bytes requested per block (0 default);
                                    used only to cap resident blocks per CU (occupancy) */
 };

@@ -85,7 +85,7 @@ struct gdp_ctx {
     float* d_taps = nullptr;
     int conv_kernel = 0;          // GDP_TUNE_CONV_KERNEL: 0 register sweep (default), 1 LDS tiles
     int conv_rows = 16;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep
-    int conv_order = 5;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
+    int conv_order = 5;           // GDP_TUNE_CONV_ORDER (default set per geometry in gdp_create): bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
                                   // bit 2 input-row-interleaved octaves (conv_sweep_perm)
     int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
@@ -362,6 +362,14 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     if (!c) return fail(GDP_ERR_NOMEM, "host allocation failed");
     c->device = device;
     c->variant = default_variant(W, (long long)(row_end - row_begin) * W, batch);
+    // Convolution-extension block order (tools/tune.py --op conv, cold buffers): batches 5 (XCD-
+    // chunked + octave rows after the octave-0 rows that hold their inputs: 64 x 4096^2 6.28 vs
+    // 7.00 ms linear), one large image 4 (the interleave without XCD chunking: 16384^2 1.59 vs
+    // 1.80 for 5), one image <= 64 Mpix 0 (linear: 4096^2 0.119 vs 0.128 for 5).
+    {
+        const long long px = (long long)(row_end - row_begin) * W;
+        c->conv_order = batch > 1 ? 5 : (px >= (1ll << 26) ? 4 : 0);
+    }
     c->cus = std::max(1, prop.multiProcessorCount);
     c->blocks_max = c->cus * 8;
     Geom& g = c->geom;
