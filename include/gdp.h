@@ -154,9 +154,10 @@ int gdp_download_level(gdp_ctx* ctx, int b, int octave, int scale, float* host);
  * float**** GaussPy[o][s] rows (GuassDePyramid.h:16) (blocking). */
 int gdp_download_level_rows(gdp_ctx* ctx, int b, int octave, int scale, float* const* rows);
 /* Mirror image b's whole pyramid into the reference's host layout GaussPy[o][s][row] (the
- * float**** of GuassDePyramid.h:16; rows as held by this context), staging every level through
- * one pinned buffer with one stream sync per 64 MiB (blocking).  What the drop-in classes call
- * after each mutating method. */
+ * float**** of GuassDePyramid.h:16; rows as held by this context), staging the levels through a
+ * double-buffered pinned buffer (the D2H copy of one 32 MiB batch overlaps the host scatter of the
+ * previous one; GDP_TUNE_STAGE_KB / _THREADS) (blocking).  What the drop-in classes call after
+ * each mutating method. */
 int gdp_download_pyramid_rows(gdp_ctx* ctx, int b, float* const* const* const* gauss_py);
 /* Copy rows [first_row, first_row + nrows) of level (o, s) of image b (rows as held by this
  * context; a band context's row 0 is its first row) to a dense host array (blocking).  Reads one
@@ -206,8 +207,12 @@ enum {
                                    o's block rows issued right after the octave-0 rows covering
                                    their input rows; default 5 for batches, 4 for one
                                    image >= 64 Mpix, 0 for smaller single images */
-    GDP_TUNE_BUILD_LDS = 12     /* gdp_build: dynamic LDS bytes requested per block (0 default);
+    GDP_TUNE_BUILD_LDS = 12,    /* gdp_build: dynamic LDS bytes requested per block (0 default);
                                    used only to cap resident blocks per CU (occupancy) */
+    GDP_TUNE_STAGE_KB = 13,     /* row-pointer downloads: KiB per half of the double-buffered
+                                   pinned staging buffer (32768 default) */
+    GDP_TUNE_STAGE_THREADS = 14 /* row-pointer downloads: host threads scattering a staged batch
+                                   into the caller's rows (4 default) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

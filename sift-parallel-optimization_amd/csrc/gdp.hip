@@ -25,6 +25,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -93,8 +94,11 @@ struct gdp_ctx {
     unsigned* d_conv_perm = nullptr; // conv sweep block order for GDP_TUNE_CONV_ORDER bit 2 (per image)
     bool conv_perm_dirty = true;
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
-    float* h_stage = nullptr;     // pinned staging for row-pointer downloads (largest level)
+    float* h_stage = nullptr;     // pinned staging for row-pointer downloads (two halves)
     size_t h_stage_floats = 0;
+    size_t stage_half_floats = kStageFloats / 2; // GDP_TUNE_STAGE_KB
+    int stage_threads = 4;        // GDP_TUNE_STAGE_THREADS: host threads scattering a staged batch
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     unsigned long long* d_sum = nullptr;
     std::vector<float> h_taps;
     long long in_pitch_own = 0, in_img_stride_own = 0;
@@ -500,6 +504,8 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_cradius) (void)hipFree(c->d_cradius);
     if (c->d_conv_perm) (void)hipFree(c->d_conv_perm);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    for (hipEvent_t e : c->ev_stage)
+        if (e) (void)hipEventDestroy(e);
     if (c->d_sum) (void)hipFree(c->d_sum);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -737,29 +743,95 @@ int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) {
     return GDP_OK;
 }
 
+// Row-pointer downloads (the drop-in class's float**** mirror): device levels -> pinned staging ->
+// the caller's rows.  The pinned buffer is split in two halves: batch k's D2H copies go into half
+// k % 2 while the host scatters batch k-1 out of the other half, so the PCIe copy and the host
+// memcpy overlap; a large batch is scattered by `stage_threads` host threads.
+struct StagePiece {
+    const float* src;      // device rows [0, nrows) of a level slice, `cols` floats each
+    size_t cols, nrows;
+    float* const* rows;    // the caller's destination row pointers for those rows
+    size_t off;            // float offset in the staging half
+};
+
+void scatter_batch(const float* half, const std::vector<StagePiece>& batch, size_t floats, int threads) {
+    auto part = [&](int t, int nt) {
+        for (const StagePiece& q : batch) {
+            const size_t r0 = q.nrows * t / nt, r1 = q.nrows * (t + 1) / nt;
+            for (size_t r = r0; r < r1; ++r) std::memcpy(q.rows[r], half + q.off + r * q.cols, q.cols * 4);
+        }
+    };
+    // threads pay off only for batches of several MiB (spawn cost ~20-50 us each)
+    const int nt = floats >= (size_t(1) << 20) ? std::max(1, threads) : 1;
+    if (nt == 1) return part(0, 1);
+    std::vector<std::thread> pool;
+    pool.reserve(nt - 1);
+    for (int t = 1; t < nt; ++t) pool.emplace_back(part, t, nt);
+    part(0, nt);
+    for (std::thread& th : pool) th.join();
+}
+
+int stage_download(gdp_ctx* c, const std::vector<StagePiece>& pieces) {
+    size_t total = 0, max_cols = 1;
+    for (const StagePiece& q : pieces) {
+        total += q.cols * q.nrows;
+        max_cols = std::max(max_cols, q.cols);
+    }
+    if (total == 0) return GDP_OK;
+    // one half holds at least one row; a download that fits one half uses a single buffer
+    size_t half = std::max(c->stage_half_floats, max_cols);
+    const bool dbl = total > half;
+    if (!dbl) half = total;
+    const size_t need = dbl ? 2 * half : half;
+    if (c->h_stage_floats < need) {
+        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->h_stage_floats = 0;
+        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, need * 4, hipHostMallocDefault));
+        c->h_stage_floats = need;
+    }
+    for (hipEvent_t& e : c->ev_stage)
+        if (!e) GDP_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // cut the pieces into batches of at most `half` floats (whole rows)
+    std::vector<std::vector<StagePiece>> batches(1);
+    std::vector<size_t> used(1, 0);
+    for (const StagePiece& q : pieces) {
+        for (size_t r = 0; r < q.nrows;) {
+            size_t fit = (half - used.back()) / q.cols;
+            if (fit == 0) {
+                batches.emplace_back();
+                used.push_back(0);
+                fit = half / q.cols;
+            }
+            const size_t nr = std::min(fit, q.nrows - r);
+            batches.back().push_back({q.src + r * q.cols, q.cols, nr, q.rows + r, used.back()});
+            used.back() += nr * q.cols;
+            r += nr;
+        }
+    }
+    const size_t nb = batches.size();
+    for (size_t k = 0; k <= nb; ++k) {
+        if (k < nb) {  // half k % 2 was scattered (batch k-2) before this iteration started
+            float* dst = c->h_stage + (k & 1) * half;
+            for (const StagePiece& q : batches[k])
+                GDP_HIP(c, hipMemcpyAsync(dst + q.off, q.src, q.cols * q.nrows * 4, hipMemcpyDeviceToHost, c->stream));
+            GDP_HIP(c, hipEventRecord(c->ev_stage[k & 1], c->stream));
+        }
+        if (k > 0) {  // batch k-1 lands while batch k is in flight
+            const size_t j = k - 1;
+            GDP_HIP(c, hipEventSynchronize(c->ev_stage[j & 1]));
+            scatter_batch(c->h_stage + (j & 1) * half, batches[j], used[j], c->stage_threads);
+        }
+    }
+    return GDP_OK;
+}
+
 int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows) {
     if (!valid_level(c, b, o, s) || !rows) return c ? c->status(GDP_ERR_ARG, "gdp_download_level_rows: bad argument") : GDP_ERR_ARG;
     const OctGeom& og = c->geom.oct[o];
     if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
-    // one pinned staging buffer of at most kStageFloats (or one row), reused chunk by chunk
-    const size_t chunk_rows = std::max<size_t>(1, std::min<size_t>(og.rows, kStageFloats / (size_t)og.cols));
-    const size_t nfl = chunk_rows * og.cols;
-    if (c->h_stage_floats < nfl) {
-        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
-        c->h_stage = nullptr;
-        c->h_stage_floats = 0;
-        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, nfl * 4, hipHostMallocDefault));
-        c->h_stage_floats = nfl;
-    }
-    const float* src = gdp_device_level(c, b, o, s);
-    for (size_t r0 = 0; r0 < (size_t)og.rows; r0 += chunk_rows) {
-        const size_t nr = std::min(chunk_rows, (size_t)og.rows - r0);
-        GDP_HIP(c, hipMemcpyAsync(c->h_stage, src + r0 * og.cols, nr * og.cols * 4, hipMemcpyDeviceToHost, c->stream));
-        GDP_HIP(c, hipStreamSynchronize(c->stream));
-        for (size_t r = 0; r < nr; ++r) std::memcpy(rows[r0 + r], c->h_stage + r * og.cols, (size_t)og.cols * 4);
-    }
-    return GDP_OK;
+    return stage_download(c, {{gdp_device_level(c, b, o, s), (size_t)og.cols, (size_t)og.rows, rows, 0}});
 }
 
 int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py) {
@@ -767,56 +839,14 @@ int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid_rows: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     const Geom& g = c->geom;
-    // levels are gathered into one pinned staging buffer (<= kStageFloats, or one level) with one
-    // stream sync per fill, then scattered into the caller's rows; a level larger than the
-    // staging buffer goes through the row-chunked gdp_download_level_rows
-    size_t cap = 0;
-    for (int o = 0; o < g.O; ++o) cap += (size_t)g.oct[o].rows * g.oct[o].cols * g.L;
-    cap = std::min(cap, kStageFloats);
-    if (cap == 0) return GDP_OK;
-    if (c->h_stage_floats < cap) {
-        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
-        c->h_stage = nullptr;
-        c->h_stage_floats = 0;
-        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, cap * 4, hipHostMallocDefault));
-        c->h_stage_floats = cap;
-    }
-    struct Pending { int o, s; size_t off; };
-    std::vector<Pending> pend;
-    size_t used = 0;
-    auto flush = [&]() -> int {
-        if (pend.empty()) return GDP_OK;
-        GDP_HIP(c, hipStreamSynchronize(c->stream));
-        for (const Pending& q : pend) {
-            const OctGeom& og = g.oct[q.o];
-            for (int r = 0; r < og.rows; ++r)
-                std::memcpy(py[q.o][q.s][r], c->h_stage + q.off + (size_t)r * og.cols, (size_t)og.cols * 4);
-        }
-        pend.clear();
-        used = 0;
-        return GDP_OK;
-    };
+    std::vector<StagePiece> pieces;
     for (int o = 0; o < g.O; ++o) {
         const OctGeom& og = g.oct[o];
-        const size_t n = (size_t)og.rows * og.cols;
-        for (int s = 0; s < g.L && n; ++s) {
-            if (n > c->h_stage_floats) {  // does not fit: row-chunked path
-                int rc = flush();
-                if (rc == GDP_OK) rc = gdp_download_level_rows(c, b, o, s, py[o][s]);
-                if (rc != GDP_OK) return rc;
-                continue;
-            }
-            if (used + n > c->h_stage_floats) {
-                const int rc = flush();
-                if (rc != GDP_OK) return rc;
-            }
-            GDP_HIP(c, hipMemcpyAsync(c->h_stage + used, gdp_device_level(c, b, o, s), n * 4, hipMemcpyDeviceToHost,
-                                      c->stream));
-            pend.push_back({o, s, used});
-            used += n;
-        }
+        if ((size_t)og.rows * og.cols == 0) continue;
+        for (int s = 0; s < g.L; ++s)
+            pieces.push_back({gdp_device_level(c, b, o, s), (size_t)og.cols, (size_t)og.rows, py[o][s], 0});
     }
-    return flush();
+    return stage_download(c, pieces);
 }
 
 int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int nrows, float* host) {
@@ -968,6 +998,8 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
+        case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
+        case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 }
@@ -1016,6 +1048,14 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
         case GDP_TUNE_BUILD_LDS:
             if (value < 0 || value > 160 * 1024) return c->status(GDP_ERR_ARG, "build LDS bytes must be in [0, 163840]");
             c->build_lds = value;
+            return GDP_OK;
+        case GDP_TUNE_STAGE_KB:
+            if (value < 1 || value > 1024 * 1024) return c->status(GDP_ERR_ARG, "staging KiB must be in [1, 1048576]");
+            c->stage_half_floats = (size_t)value * 256;
+            return GDP_OK;
+        case GDP_TUNE_STAGE_THREADS:
+            if (value < 1 || value > 64) return c->status(GDP_ERR_ARG, "staging threads must be in [1, 64]");
+            c->stage_threads = value;
             return GDP_OK;
         case GDP_TUNE_TILE_ORDER:
             if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");

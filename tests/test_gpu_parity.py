@@ -433,11 +433,19 @@ def test_pyramid_rows_mirror(pkg, oracle):
 
     from sift_parallel_optimization_amd import _lib
 
-    for H, W, S, B, band in [(96, 160, 2, 1, None), (100, 37, 3, 2, None), (256, 300, 2, 1, (16, 48))]:
+    # the last cases shrink the double-buffered staging to 1 KiB per half (256 floats: many
+    # batches, pieces split across batches, rows wider than a half) and vary the scatter threads
+    cases = [(96, 160, 2, 1, None, None), (100, 37, 3, 2, None, None), (256, 300, 2, 1, (16, 48), None),
+             (96, 160, 2, 1, None, (1, 1)), (100, 37, 3, 2, None, (1, 3)), (256, 300, 2, 1, (16, 48), (1, 2)),
+             (1100, 1000, 2, 1, None, (64, 3)), (1100, 1000, 2, 1, None, (4096, 3))]
+    for H, W, S, B, band, stage in cases:
         kw = dict(row_begin=band[0], row_end=band[1]) if band else {}
         with pkg.PyramidContext(H, W, S=S, batch=B, octaves=5 if band else 0, **kw) as ctx:
             ctx.fill_synthetic(0x5EED, 2)
             ctx.build()
+            if stage:
+                ctx.set_tuning(stage_kb=stage[0], stage_threads=stage[1])
+                assert ctx.tuning()["stage_kb"] == stage[0] and ctx.tuning()["stage_threads"] == stage[1]
             b = B - 1
             rows = {}
             top = (ctypes.c_void_p * ctx.O)()

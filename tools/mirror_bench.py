@@ -1,0 +1,66 @@
+"""Host-mirror (PCIe-inclusive) timing of gdp_download_pyramid_rows: device pyramid -> the
+reference's float**** GaussPy rows (what GaussPyramid_hip does after every mutating call).
+
+    python tools/mirror_bench.py [--n 4096] [--reps 5] [--stage "32768x1,32768x4,..."]
+
+Each setting is `<KiB per staging half>x<scatter threads>`; prints ms and GB/s per download
+(median of --reps after one warm-up, which also first-touches the destination rows)."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import __graft_entry__ as entry  # noqa: E402
+
+pkg = entry.load_package()
+_lib = sys.modules["sift_parallel_optimization_amd._lib"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--S", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--stage", default="1048576x1,1048576x4,32768x1,32768x2,32768x4,32768x8,8192x4,131072x4")
+    a = ap.parse_args()
+    with pkg.PyramidContext(a.n, a.n, S=a.S, octaves=0) as ctx:
+        ctx.fill_synthetic(0x5EED, 0)
+        ctx.build()
+        ctx.sync()
+        top = (ctypes.c_void_p * ctx.O)()
+        keep, nbytes = [], 0
+        for o in range(ctx.O):
+            nr, nc, _ = ctx.level_dims(o)
+            lev = (ctypes.c_void_p * (a.S + 3))()
+            for s in range(a.S + 3):
+                arr = np.empty((max(nr, 1), nc), np.float32)
+                rp = (ctypes.c_void_p * max(nr, 1))(*[arr[r].ctypes.data for r in range(max(nr, 1))])
+                keep.append((arr, rp))
+                lev[s] = ctypes.cast(rp, ctypes.c_void_p)
+                nbytes += 4 * nr * nc
+            keep.append(lev)
+            top[o] = ctypes.cast(lev, ctypes.c_void_p)
+        want = [ctx.level(0, o, s) for o in range(min(ctx.O, 2)) for s in range(a.S + 3)]
+        for spec in a.stage.split(","):
+            kb, th = (int(x) for x in spec.split("x"))
+            ctx.set_tuning(stage_kb=kb, stage_threads=th)
+            ts = []
+            for r in range(a.reps + 1):
+                t0 = time.perf_counter()
+                _lib.check(_lib.lib().gdp_download_pyramid_rows(ctx._ctx, 0, top), ctx._ctx)
+                ts.append(time.perf_counter() - t0)
+            got = [keep[o * (a.S + 4) + s][0][: ctx.level_dims(o)[0]] for o in range(min(ctx.O, 2))
+                   for s in range(a.S + 3)]
+            ok = all(np.array_equal(g.view(np.uint32), w.view(np.uint32)) for g, w in zip(got, want))
+            ms = 1e3 * float(np.median(ts[1:]))
+            print(json.dumps({"n": a.n, "stage_kb": kb, "threads": th, "ms": round(ms, 3),
+                              "GB/s": round(nbytes / ms / 1e6, 2), "bytes": nbytes, "exact": ok}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
