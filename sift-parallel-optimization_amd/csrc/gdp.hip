@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <new>
 #include <string>
 #include <thread>
@@ -586,17 +587,39 @@ int gdp_set_input_host_u8(gdp_ctx* c, int b, const uint8_t* base, size_t pitch, 
     return upload_input(c, b, base, pitch, GDP_INPUT_U8, stream, "gdp_set_input_host_u8");
 }
 
+static int ensure_stage(gdp_ctx* c, size_t floats);
+static void parallel_rows(size_t nrows, size_t floats, int threads, const std::function<void(size_t, size_t)>& fn);
+
 int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stream) {
     if (!c || !rows || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_set_input_rows: bad argument") : GDP_ERR_ARG;
     if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
-    // Gather the row pointers into one staging image, then one 2-D copy.
-    const size_t W = (size_t)c->geom.W, R = (size_t)c->geom.in_rows;
-    std::vector<int32_t> stage(W * R);
-    for (size_t r = 0; r < R; ++r) {
+    if (c->geom.in_fmt != GDP_INPUT_I32)
+        return c->status(GDP_ERR_STATE, "gdp_set_input_rows: context input format differs (gdp_set_input_format)");
+    const size_t W = (size_t)c->geom.W, R = (size_t)c->geom.in_rows, pitch = (size_t)c->geom.in_pitch;
+    for (size_t r = 0; r < R; ++r)
         if (!rows[r]) return c->status(GDP_ERR_ARG, "gdp_set_input_rows: null row %zu", r);
-        std::memcpy(stage.data() + r * W, rows[r], W * 4);
+    if (W * R == 0) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    hipStream_t st = c->pick(stream);
+    // The rows are gathered into the double-buffered pinned staging (the mirror of
+    // stage_download): the host gathers batch k into one half while batch k-1's 2-D copy runs.
+    const size_t per = std::max<size_t>(1, std::min(R, c->stage_half_floats / W)), half = per * W;
+    const size_t nb = (R + per - 1) / per;
+    const int rc = ensure_stage(c, nb > 1 ? 2 * half : half);
+    if (rc != GDP_OK) return rc;
+    int32_t* dst = static_cast<int32_t*>(c->d_in_own) + (size_t)b * c->geom.in_img_stride;
+    for (size_t k = 0; k < nb; ++k) {
+        int32_t* h = reinterpret_cast<int32_t*>(c->h_stage) + (k & 1) * half;
+        if (k >= 2) GDP_HIP(c, hipEventSynchronize(c->ev_stage[k & 1]));  // batch k-2 has left this half
+        const size_t r0 = k * per, nr = std::min(per, R - r0);
+        parallel_rows(nr, nr * W, c->stage_threads, [&](size_t a, size_t e) {
+            for (size_t r = a; r < e; ++r) std::memcpy(h + r * W, rows[r0 + r], W * 4);
+        });
+        GDP_HIP(c, hipMemcpy2DAsync(dst + r0 * pitch, pitch * 4, h, W * 4, W * 4, nr, hipMemcpyHostToDevice, st));
+        GDP_HIP(c, hipEventRecord(c->ev_stage[k & 1], st));
     }
-    return gdp_set_input_host(c, b, stage.data(), W, stream);
+    GDP_HIP(c, hipStreamSynchronize(st));
+    return GDP_OK;
 }
 
 int gdp_set_input_device(gdp_ctx* c, const int32_t* base, size_t pitch, size_t image_stride) {
@@ -754,24 +777,45 @@ struct StagePiece {
     size_t off;            // float offset in the staging half
 };
 
-void scatter_batch(const float* half, const std::vector<StagePiece>& batch, size_t floats, int threads) {
-    auto part = [&](int t, int nt) {
-        for (const StagePiece& q : batch) {
-            const size_t r0 = q.nrows * t / nt, r1 = q.nrows * (t + 1) / nt;
-            for (size_t r = r0; r < r1; ++r) std::memcpy(q.rows[r], half + q.off + r * q.cols, q.cols * 4);
-        }
-    };
-    // threads pay off only for batches of several MiB (spawn cost ~20-50 us each)
-    const int nt = floats >= (size_t(1) << 20) ? std::max(1, threads) : 1;
-    if (nt == 1) return part(0, 1);
+// Runs fn(r0, r1) over [0, nrows) on `threads` host threads (one thread below 1 M floats: the
+// spawn cost, ~20-50 us a thread, only pays off for batches of several MiB).
+static void parallel_rows(size_t nrows, size_t floats, int threads, const std::function<void(size_t, size_t)>& fn) {
+    const size_t nt = floats >= (size_t(1) << 20) ? std::min<size_t>(std::max(1, threads), nrows) : 1;
+    if (nt <= 1) return fn(0, nrows);
     std::vector<std::thread> pool;
     pool.reserve(nt - 1);
-    for (int t = 1; t < nt; ++t) pool.emplace_back(part, t, nt);
-    part(0, nt);
+    for (size_t t = 1; t < nt; ++t) pool.emplace_back(fn, nrows * t / nt, nrows * (t + 1) / nt);
+    fn(0, nrows / nt);
     for (std::thread& th : pool) th.join();
 }
 
-int stage_download(gdp_ctx* c, const std::vector<StagePiece>& pieces) {
+static void scatter_batch(const float* half, const std::vector<StagePiece>& batch, size_t floats, int threads) {
+    size_t rows = 0;
+    for (const StagePiece& q : batch) rows = std::max(rows, q.nrows);
+    // thread t takes the same fraction of every piece's rows
+    parallel_rows(rows, floats, threads, [&](size_t a, size_t e) {
+        for (const StagePiece& q : batch) {
+            const size_t r0 = q.nrows * a / rows, r1 = q.nrows * e / rows;
+            for (size_t r = r0; r < r1; ++r) std::memcpy(q.rows[r], half + q.off + r * q.cols, q.cols * 4);
+        }
+    });
+}
+
+// The pinned staging buffer (floats) and its two half-events, grown on demand.
+static int ensure_stage(gdp_ctx* c, size_t need) {
+    if (c->h_stage_floats < need) {
+        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->h_stage_floats = 0;
+        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, need * 4, hipHostMallocDefault));
+        c->h_stage_floats = need;
+    }
+    for (hipEvent_t& e : c->ev_stage)
+        if (!e) GDP_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return GDP_OK;
+}
+
+static int stage_download(gdp_ctx* c, const std::vector<StagePiece>& pieces) {
     size_t total = 0, max_cols = 1;
     for (const StagePiece& q : pieces) {
         total += q.cols * q.nrows;
@@ -782,16 +826,8 @@ int stage_download(gdp_ctx* c, const std::vector<StagePiece>& pieces) {
     size_t half = std::max(c->stage_half_floats, max_cols);
     const bool dbl = total > half;
     if (!dbl) half = total;
-    const size_t need = dbl ? 2 * half : half;
-    if (c->h_stage_floats < need) {
-        if (c->h_stage) GDP_HIP(c, hipHostFree(c->h_stage));
-        c->h_stage = nullptr;
-        c->h_stage_floats = 0;
-        GDP_HIP(c, hipHostMalloc((void**)&c->h_stage, need * 4, hipHostMallocDefault));
-        c->h_stage_floats = need;
-    }
-    for (hipEvent_t& e : c->ev_stage)
-        if (!e) GDP_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const int rc = ensure_stage(c, dbl ? 2 * half : half);
+    if (rc != GDP_OK) return rc;
     // cut the pieces into batches of at most `half` floats (whole rows)
     std::vector<std::vector<StagePiece>> batches(1);
     std::vector<size_t> used(1, 0);

@@ -274,6 +274,23 @@ def test_int_star_star_upload(pkg, oracle):
         ctx.set_input_rows([img[r] for r in range(40)])
         ctx.build()
         _assert_same(ctx.pyramid(0), oracle.build_pyramid(img, 2), "int** upload")
+    # double-buffered pinned staging: tiny halves (many batches, one row per batch when a row is
+    # wider than a half), threaded gathers, a batch image and a row band, against the packed upload
+    big = oracle.lcg_image(1100, 1000, 5)
+    for kb, th, B, band in [(1, 1, 1, None), (1, 3, 2, None), (4096, 3, 2, None), (2, 2, 1, (64, 320))]:
+        H, W = (1100, 1000) if band is None else (1024, 1000)
+        kw = dict(row_begin=band[0], row_end=band[1], octaves=5) if band else {}
+        lo, hi = band if band else (0, H)
+        with pkg.PyramidContext(H, W, S=2, batch=B, **kw) as a, pkg.PyramidContext(H, W, S=2, batch=B, **kw) as ref:
+            a.set_tuning(stage_kb=kb, stage_threads=th)
+            for bi in range(B):
+                r_img = np.ascontiguousarray(big[lo:hi, :W] + bi)
+                a.set_input_rows([r_img[r] for r in range(hi - lo)], b=bi)
+                ref.set_input(r_img, b=bi)
+            a.build()
+            ref.build()
+            for bi in range(B):
+                assert a.checksum(bi) == ref.checksum(bi), ("int** staged", kb, th, bi, band)
 
 
 # ------------------------------------------------------------------ in-place ops / re-entry

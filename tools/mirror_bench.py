@@ -1,4 +1,5 @@
-"""Host-mirror (PCIe-inclusive) timing of gdp_download_pyramid_rows: device pyramid -> the
+"""Host-mirror (PCIe-inclusive) timing of gdp_download_pyramid_rows (and of the int** upload,
+gdp_set_input_rows): device pyramid -> the
 reference's float**** GaussPy rows (what GaussPyramid_hip does after every mutating call).
 
     python tools/mirror_bench.py [--n 4096] [--reps 5] [--stage "32768x1,32768x4,..."]
@@ -60,6 +61,26 @@ def main():
             ms = 1e3 * float(np.median(ts[1:]))
             print(json.dumps({"n": a.n, "stage_kb": kb, "threads": th, "ms": round(ms, 3),
                               "GB/s": round(nbytes / ms / 1e6, 2), "bytes": nbytes, "exact": ok}), flush=True)
+        # the other direction: the reference ctor's int** image -> device (gdp_set_input_rows)
+        img = (np.arange(a.n * a.n, dtype=np.int64).reshape(a.n, a.n) * 2654435761 % 251).astype(np.int32)
+        rows = [img[r] for r in range(a.n)]
+        ptrs = (ctypes.c_void_p * a.n)(*[r.ctypes.data for r in rows])
+        ref_sum = None
+        for spec in a.stage.split(","):
+            kb, th = (int(x) for x in spec.split("x"))
+            ctx.set_tuning(stage_kb=kb, stage_threads=th)
+            ts = []
+            for r in range(a.reps + 1):
+                t0 = time.perf_counter()
+                _lib.check(_lib.lib().gdp_set_input_rows(ctx._ctx, 0, ptrs, None), ctx._ctx)
+                ts.append(time.perf_counter() - t0)
+            ctx.build()
+            cs = ctx.checksum(0)
+            ref_sum = cs if ref_sum is None else ref_sum
+            ms = 1e3 * float(np.median(ts[1:]))
+            print(json.dumps({"upload_n": a.n, "stage_kb": kb, "threads": th, "ms": round(ms, 3),
+                              "GB/s": round(4 * a.n * a.n / ms / 1e6, 2), "same_checksum": cs == ref_sum}),
+                  flush=True)
 
 
 if __name__ == "__main__":
