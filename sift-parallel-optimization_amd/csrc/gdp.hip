@@ -848,9 +848,17 @@ static int stage_download(gdp_ctx* c, const std::vector<StagePiece>& pieces) {
     const size_t nb = batches.size();
     for (size_t k = 0; k <= nb; ++k) {
         if (k < nb) {  // half k % 2 was scattered (batch k-2) before this iteration started
+            // pieces adjacent both on the device and in the half (the levels of one image are packed
+            // [o][s][r][c]) go as one copy: a small pyramid is one DMA, not one per level
             float* dst = c->h_stage + (k & 1) * half;
-            for (const StagePiece& q : batches[k])
-                GDP_HIP(c, hipMemcpyAsync(dst + q.off, q.src, q.cols * q.nrows * 4, hipMemcpyDeviceToHost, c->stream));
+            const std::vector<StagePiece>& bk = batches[k];
+            for (size_t i = 0; i < bk.size();) {
+                size_t n = bk[i].cols * bk[i].nrows, j = i + 1;
+                for (; j < bk.size() && bk[j].src == bk[i].src + n && bk[j].off == bk[i].off + n; ++j)
+                    n += bk[j].cols * bk[j].nrows;
+                GDP_HIP(c, hipMemcpyAsync(dst + bk[i].off, bk[i].src, n * 4, hipMemcpyDeviceToHost, c->stream));
+                i = j;
+            }
             GDP_HIP(c, hipEventRecord(c->ev_stage[k & 1], c->stream));
         }
         if (k > 0) {  // batch k-1 lands while batch k is in flight
