@@ -463,6 +463,9 @@ def test_pyramid_rows_mirror(pkg, oracle):
             if stage:
                 ctx.set_tuning(stage_kb=stage[0], stage_threads=stage[1])
                 assert ctx.tuning()["stage_kb"] == stage[0] and ctx.tuning()["stage_threads"] == stage[1]
+                for bad in (dict(stage_kb=0), dict(stage_kb=1 << 21), dict(stage_threads=0), dict(stage_threads=65)):
+                    with pytest.raises(pkg.GdpError):
+                        ctx.set_tuning(**bad)
             b = B - 1
             rows = {}
             top = (ctypes.c_void_p * ctx.O)()
