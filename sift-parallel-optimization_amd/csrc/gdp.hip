@@ -783,8 +783,13 @@ static void parallel_rows(size_t nrows, size_t floats, int threads, const std::f
     const size_t nt = floats >= (size_t(1) << 20) ? std::min<size_t>(std::max(1, threads), nrows) : 1;
     if (nt <= 1) return fn(0, nrows);
     std::vector<std::thread> pool;
-    pool.reserve(nt - 1);
-    for (size_t t = 1; t < nt; ++t) pool.emplace_back(fn, nrows * t / nt, nrows * (t + 1) / nt);
+    size_t t = 1;
+    try {  // no exception may cross the C ABI: parts whose thread could not start run here
+        pool.reserve(nt - 1);
+        for (; t < nt; ++t) pool.emplace_back(fn, nrows * t / nt, nrows * (t + 1) / nt);
+    } catch (...) {
+    }
+    for (; t < nt; ++t) fn(nrows * t / nt, nrows * (t + 1) / nt);
     fn(0, nrows / nt);
     for (std::thread& th : pool) th.join();
 }
