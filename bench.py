@@ -12,6 +12,12 @@ the 256 MB Infinity Cache between steps: the rate is the HBM rate.  One process 
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 
+--gpus N > 1 without a launcher (WORLD_SIZE unset) starts N rank processes itself — one per GPU,
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment — before
+anything touches the GPU, and exits with the first failing rank's status; under torchrun
+(WORLD_SIZE set) it is one of the ranks.  A world size that differs from --gpus, or more ranks
+than visible GPUs under "nccl", is an error.
+
 Workloads (BASELINE.json configs; c2 is the default, the single-GPU config the metric names):
   c2: 4096x4096, 5 octaves, 1 image per GPU per step
   c3: 64 x 1080x1920 (HxW), 5 octaves, per GPU per step (persistent kernel)
@@ -139,9 +145,11 @@ def cpu_baseline(budget_s):
                       f"median of {len(times)} calls", "cpu": cpu_info()}
 
 
-def latest_pmc(config_key):
-    """PMC-derived HBM bytes per launch for this workload, from profiles/pmc_*.json (written by
-    profiles/collect_pmc.py from separate rocprofv3 --pmc passes), or None."""
+def latest_pmc(config_key, variant, tile_order):
+    """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
+    profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
+    whose recorded build variant and tile order equal the run's; None when no profile of that
+    instance exists (the traffic of another variant would describe a different kernel)."""
     pdir = os.path.join(REPO, "profiles")
     best = None
     if os.path.isdir(pdir):
@@ -153,9 +161,53 @@ def latest_pmc(config_key):
                 except (OSError, ValueError):
                     continue
                 if rec.get("config") == config_key and rec.get("op", "build") == "build" and \
-                        rec.get("kernel_bytes_per_launch"):
-                    best = rec
+                        rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
+                        rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32":
+                    best = dict(rec, file=f)
     return best
+
+
+def launch_ranks(n, argv, script=None):
+    """`bench.py --gpus N` with no launcher: start N rank processes of this script (one per GPU)
+    and wait for them.  Runs before anything imports torch or touches the GPU; the parent never
+    does.  If a rank fails the others are stopped (they would wait in a collective forever)."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+    return rc
 
 
 def autotune_rotating(ctxs, stream, iters, rounds=5):
@@ -237,42 +289,67 @@ def scatter_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
             "GBps": round(nbytes / secs / 1e9, 1) if secs > 0 else None, "bit_exact": bad == 0.0}
 
 
-def verify(ctx, cfg, key, world, rank, dist, mg):
+def _fixture_checksums(cfg):
+    """global image index -> the gdp_checksum of the reference's output for that synthetic image
+    (tests/golden/checksums.json; square images, generated by the reference binary), or of the
+    oracle's closed form for non-square images (checksums_oracle.json: the reference only builds
+    square pyramids; the oracle is pinned to it on every square fixture, tests/test_oracle.py)."""
+    H, W, O = cfg["H"], cfg["W"], cfg["O"]
+    prefix = f"synth:{SEED:#x}:".lower()
+    out = {}
+    if H == W:
+        with open(os.path.join(REPO, "tests", "golden", "checksums.json")) as f:
+            for r in json.load(f):
+                if r["n"] == H and r["S"] == 2 and r["input"].lower().startswith(prefix) and f"octaves_{O}" in r:
+                    out[int(r["input"].split(":")[2])] = (int(r[f"octaves_{O}"], 16), "reference")
+    else:
+        with open(os.path.join(REPO, "tests", "golden", "checksums_oracle.json")) as f:
+            for r in json.load(f):
+                if (r["H"], r["W"], r["S"], r["octaves"]) == (H, W, 2, O) and r["input"].lower().startswith(prefix):
+                    out[int(r["input"].split(":")[2])] = (int(r["checksum"], 16), "oracle")
+    return out
+
+
+def verify(ctx, cfg, key, world, rank, dist, mg, first_image):
     """After the timed region: gdp_checksum of what the benchmark built vs the checksum of the
-    reference's own output for the same input (tests/golden/checksums.json).  Image configs check
-    global image 0 (rank 0); the row-band config sums every rank's band checksum."""
-    path = os.path.join(REPO, "tests", "golden", "checksums.json")
-    with open(path) as f:
-        fixtures = {(r["n"], r["input"].lower()): r for r in json.load(f)}
-    H, O = cfg["H"], cfg["O"]
-    rec = fixtures.get((H, f"synth:{SEED:#x}:0".lower())) if cfg["H"] == cfg["W"] else None
+    reference's own output for the same input.  Image configs: EVERY rank checksums the first and
+    last image of its shard and rank 0 checks each against the fixtures (tests/golden/), so an
+    N-rank line certifies every rank's images; the row-band config sums every rank's band
+    checksum into the image's."""
+    fixtures = _fixture_checksums(cfg)
     if cfg["band"]:
         sums = mg.gather_checksums([ctx.checksum(0)], dist=dist)
         if rank != 0:
             return None
         got = sum(v[0] for v in sums) & 0xFFFFFFFFFFFFFFFF
-        what = f"sum of {world} row-band checksums"
-    else:
-        if rank != 0:
-            return None
-        got = ctx.checksum(0)
-        what = "global image 0"
-    if rec is None and cfg["H"] != cfg["W"]:
-        # non-square (config 3): the reference only builds square images; the fixture is the
-        # oracle's closed form, pinned to the reference on every square fixture
-        # (tests/golden/gen_oracle_checksums.py, tests/test_oracle.py)
-        with open(os.path.join(REPO, "tests", "golden", "checksums_oracle.json")) as f:
-            for r in json.load(f):
-                if (r["H"], r["W"], r["octaves"], r["input"].lower()) == (H, cfg["W"], O, f"synth:{SEED:#x}:0"):
-                    want = int(r["checksum"], 16)
-                    return {"status": "bit-exact" if got == want else "MISMATCH", "checked": what,
-                            "checksum": f"{got:016x}", "oracle_checksum": f"{want:016x}",
-                            "against": "oracle closed form (non-square input: no reference output exists)"}
-    if rec is None or f"octaves_{O}" not in rec:
-        return {"status": "unchecked (no reference fixture for this input)", "checksum": f"{got:016x}"}
-    want = int(rec[f"octaves_{O}"], 16)
-    return {"status": "bit-exact" if got == want else "MISMATCH", "checked": what,
-            "checksum": f"{got:016x}", "reference_checksum": f"{want:016x}"}
+        want = fixtures.get(0)
+        if want is None:
+            return {"status": "unchecked (no reference fixture for this input)", "checksum": f"{got:016x}"}
+        return {"status": "bit-exact" if got == want[0] else "MISMATCH",
+                "checked": f"sum of {world} row-band checksums = image 0", "checksum": f"{got:016x}",
+                "reference_checksum": f"{want[0]:016x}"}
+    B = cfg["batch"]
+    local = sorted({0, B - 1})
+    mine = [[first_image + b, ctx.checksum(b)] for b in local]
+    per_rank = mg.gather_checksums([v for pair in mine for v in pair], dist=dist)
+    if rank != 0:
+        return None
+    checked, unchecked, bad = [], [], []
+    for r, flat in enumerate(per_rank):
+        for idx, got in zip(flat[0::2], flat[1::2]):
+            want = fixtures.get(int(idx))
+            if want is None:
+                unchecked.append(int(idx))
+                continue
+            (checked if got == want[0] else bad).append(int(idx))
+    status = "MISMATCH" if bad else ("bit-exact" if checked else "unchecked (no fixture for these images)")
+    against = {v[1] for v in fixtures.values()}
+    return {"status": status,
+            "checked": f"first and last image of each of {world} rank(s): global images {sorted(checked + bad)}",
+            "bit_exact_images": len(checked), "mismatched_images": bad, "images_without_fixture": unchecked,
+            "ranks_certified": sorted({i // B for i in checked} - {i // B for i in bad}),
+            "against": ("reference output (tests/golden/checksums.json)" if against == {"reference"} else
+                        "oracle closed form (non-square input: no reference output exists)")}
 
 
 def main():
@@ -305,20 +382,28 @@ def main():
                     help="independent input+pyramid buffer sets the steps cycle through (default: enough to "
                          "exceed %d MiB, so no step finds its lines in the 256 MB Infinity Cache)" % (ROTATE_BYTES >> 20))
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, before torch is imported or a GPU is touched
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
 
     import __graft_entry__ as entry
 
-    pkg = entry.load_package()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     # one process per GPU; GDP_BENCH_BACKEND=gloo lets a 1-GPU box rehearse N ranks on device 0
     backend = os.environ.get("GDP_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        sys.exit(f"bench.py: {world} ranks need {world} GPUs under nccl (RCCL), {ndev} visible "
+                 f"(GDP_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
+    pkg = entry.load_package()
     local = local if backend == "nccl" else local % max(1, ndev)
     torch.cuda.set_device(local)
     dist = None
@@ -415,7 +500,7 @@ def main():
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
     wall, kernel_ms = mg.max_over_ranks([wall, kernel_ms], dist=dist, device=red_dev)
-    parity = verify(ctx, cfg, args.config, world, rank, dist, mg) if args.op == "build" else None
+    parity = verify(ctx, cfg, args.config, world, rank, dist, mg, first_image) if args.op == "build" else None
     if parity is not None and rotate > 1:
         # every rotated set built the same images: their checksums must all equal set 0's
         sums = {c.checksum(0) for c in ctxs}
@@ -433,7 +518,8 @@ def main():
     else:
         bytes_launch = algorithmic_bytes(H, W, S, O, B, in_bytes)
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
-    pmc = latest_pmc(args.config) if args.op == "build" and args.input == "i32" else None
+    tun = ctx.tuning()
+    pmc = latest_pmc(args.config, tun["variant"], tun["tile_order"]) if args.op == "build" and args.input == "i32" else None
 
     result = {
         "metric": METRIC,
@@ -461,6 +547,9 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(pmc["kernel_bytes_per_launch"]) if pmc else None,
+            "traffic_source": (f"profiles/{pmc['file']}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same "
+                               f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}) on this workload"
+                               if pmc else "no PMC profile of this kernel instance (variant/tile order) on this workload"),
             "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d%s"
                        % (ctx.tuning()["variant"], ctx.tuning()["tile_order"], " (autotuned)" if autotuned else "")
                        if args.op == "build" else

@@ -1,7 +1,9 @@
 // main.cpp (:26-75) driving the MPI-variant drop-in (GaussDePyramid-HIP-mpi.h): all-ones MAX x MAX
 // image, n = 512, S = 2, GenerateDoG_mpi in a >= 100 ms loop, mean ms printed by the collector.
 // Launch with any MPI: `mpiexec -n <ranks> examples/mpi_hip` (one GPU per rank), or directly
-// (MPI singleton, one rank).  Parity mode: mpi_hip [n] [lcg:SEED|ones] [dump.f32]
+// (MPI singleton, one rank).  Parity mode: mpi_hip [n] [lcg:SEED|ones] [dump.f32] [calls] [mixed]
+// — `calls` GenerateDoG_mpi calls on the same object (default 1); with "mixed" a single-process
+// GenerateDoG() runs between consecutive GenerateDoG_mpi calls.
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -30,8 +32,13 @@ int main(int argc, char* argv[]) {
         }
     }
     GaussPyramid_hip_mpi g(p, n, 2);
-    if (argc > 3) {  // parity mode: one collective build, the collector dumps its GaussPy
-        g.GenerateDoG_mgpu(argc, argv);  // = GenerateDoG_mpi (the SURVEY's name for the RCCL form)
+    if (argc > 3) {  // parity mode: collective builds, the collector dumps its GaussPy
+        const int calls = argc > 4 ? std::atoi(argv[4]) : 1;
+        const bool mixed = argc > 5 && std::string(argv[5]) == "mixed";
+        for (int c = 0; c < calls; ++c) {
+            if (c > 0 && mixed) g.GenerateDoG();
+            g.GenerateDoG_mgpu(argc, argv);  // = GenerateDoG_mpi (the SURVEY's name for the RCCL form)
+        }
         if (g.rank() == 0) {
             FILE* f = std::fopen(argv[3], "wb");
             for (int o = 0, len = n; len; ++o, len /= 2)

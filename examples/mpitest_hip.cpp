@@ -1,6 +1,6 @@
 // mpitest.cpp's driver (:496-558) on the drop-in header: all-ones MAX x MAX image, n = 256,
 // GaussPyInit(p) then GenerateDoG_mpi_omp(argc, argv).  Parity mode:
-//     mpitest_hip [n] [lcg:SEED|ones] [dump.f32]
+//     mpitest_hip [n] [lcg:SEED|ones] [dump.f32] [mpi|mpi_omp] [S]
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -25,8 +25,12 @@ int main(int argc, char* argv[]) {
         }
     }
     n = nn;
+    if (argc > 5) S = std::atoi(argv[5]);
     GaussPyInit(p);
-    GenerateDoG_mpi_omp(argc, argv);
+    if (argc > 4 && std::string(argv[4]) == "mpi")
+        GenerateDoG_mpi(argc, argv);
+    else
+        GenerateDoG_mpi_omp(argc, argv);
     if (argc > 3) {
         FILE* f = std::fopen(argv[3], "wb");
         for (int o = 0; o < layer; ++o)

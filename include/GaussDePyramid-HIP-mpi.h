@@ -14,17 +14,32 @@
 // (:265-335); the collector's GaussPy ends as the full pyramid.  Here ANY number of ranks works:
 // rank r builds row band gdp_band_rows(n, size, r, layer) of every level on GPU r % devices,
 // and rank 0 — the collector — receives every band into its whole-image context and mirrors it
-// into GaussPy; other ranks' GaussPy keep their GaussPyInit contents (the reference's workers
-// also end with partial data).  Bit-identical to GuassDePyramid.h's GenerateDoG on the collector.
-// Differences: MPI is initialised once (if the caller has not) and finalised by the destructor,
-// so GenerateDoG_mpi may be called repeatedly (the reference calls MPI_Init/MPI_Finalize inside
-// and cannot); every call rebuilds from the input (a fresh GaussPyInit + GenerateDoG), i.e. what
-// one reference call produces.  Errors abort with a message instead of continuing.
+// into GaussPy; other ranks' GaussPy keep their contents (the reference's workers also end with
+// partial data).  The collector's pyramid is bit-identical to the reference's collector for EVERY
+// n: GenerateDoG_mpi centres its windows on the integer octave length (`l = float(len-1)/2`,
+// :273 — GDP_CENTRE_INTLEN), while GaussFilter/GenerateDoG use the float-halved centre of
+// :134-143 like GuassDePyramid.h (the two differ only when n is not a multiple of 2^(layer-1),
+// e.g. n = 100; pinned against the reference's own MPI runs, tests/golden/mpi_hashes.json).
+// Repeated calls continue from the current contents, like the reference's in-place methods:
+// right after GaussPyInit a call is the fused build of each band; after an earlier
+// GenerateDoG_mpi each band re-enters on its own rows (the op is pointwise, so this equals the
+// collector's whole-pyramid re-entry); after single-process calls (GaussFilter / GenerateDoG)
+// each rank applies GenerateDoG_mpi to its own GaussPy without communication — on the collector
+// that is the reference's result; workers, as in the reference, hold whatever their own calls
+// left.  Differences: MPI is initialised once (if the caller has not) and finalised by the
+// destructor, so GenerateDoG_mpi may be called repeatedly (the reference calls
+// MPI_Init/MPI_Finalize inside and cannot); errors abort with a message instead of continuing.
 #ifndef SIFT_GAUSSDEPYRAMID_HIP_MPI_H
 #define SIFT_GAUSSDEPYRAMID_HIP_MPI_H
 
 #include <mpi.h>
 
+// What a caller of the replaced header gets transitively: GaussDePyramid-MPI.h:8-13 pulls in
+// <iostream>, <chrono>, <math.h> and <sys/time.h>, and main.cpp:62-69 relies on <chrono>.
+#include <math.h>
+#include <sys/time.h>
+
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
@@ -64,6 +79,8 @@ protected:
     gdp_comm* comm_;
     int rank_, size_;
     bool owns_mpi_;
+    bool fresh_;      // contents == GaussPyInit() on every rank
+    bool band_live_;  // band_ holds this rank's rows of the last GenerateDoG_mpi result
     // the error text is read only after the failing call returned (never as a sibling argument,
     // whose evaluation order relative to the call is unspecified)
     static void check_(int status, const char* what, const gdp_ctx* c) {
@@ -86,7 +103,7 @@ protected:
 inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi()
     : data(nullptr), GaussPy(nullptr), thread_count(8), chunk_size(5), all_time(0), length(0), S(0), layer(0),
       filter(nullptr), is_initialized(false), full_(nullptr), band_(nullptr), comm_(nullptr), rank_(0), size_(1),
-      owns_mpi_(false) {}
+      owns_mpi_(false), fresh_(false), band_live_(false) {}
 
 inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi(int** img, int len, int S_) : GaussPyramid_hip_mpi() {
     length = len;
@@ -133,16 +150,20 @@ inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GP
     }
     check_(gdp_init(full_, nullptr), "GaussPyInit", full_);
     is_initialized = true;
+    fresh_ = true;
+    band_live_ = false;
     sync_host_();
 }
 
 inline void GaussPyramid_hip_mpi::GaussFilter(int theLayer) {  // :133-167
     check_(gdp_gauss_octave(full_, theLayer, nullptr), "GaussFilter", full_);
+    fresh_ = band_live_ = false;
     sync_host_();
 }
 
 inline void GaussPyramid_hip_mpi::GenerateDoG() {  // :169-183 (single process, current contents)
     check_(gdp_generate_dog(full_, nullptr), "GenerateDoG", full_);
+    fresh_ = band_live_ = false;
     sync_host_();
 }
 
@@ -167,13 +188,27 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
         if (r1 > r0) {  // more ranks than aligned bands leaves the last ranks without rows
             check_(gdp_create_band(&band_, length, length, S, layer, 1, r0, r1, device), "GenerateDoG_mpi",
                    nullptr);
+            // the variant's window centre (GaussDePyramid-MPI.h:273), see the header comment
+            check_(gdp_set_window_centre(band_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi", band_);
             check_(gdp_set_input_rows(band_, 0, (const int32_t* const*)(data + r0), nullptr), "GenerateDoG_mpi",
                    band_);
         }
     }
-    if (band_) check_(gdp_build(band_, nullptr), "GenerateDoG_mpi", band_);
+    if (!fresh_ && !band_live_) {
+        // single-process calls changed GaussPy since the last collective: every rank (all take
+        // this branch: the API is SPMD) applies GenerateDoG_mpi's filter + DoG to its own
+        // contents, the collector's being the reference's collector state
+        check_(gdp_set_window_centre(full_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi", full_);
+        check_(gdp_generate_dog(full_, nullptr), "GenerateDoG_mpi", full_);
+        check_(gdp_set_window_centre(full_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi", full_);
+        sync_host_();
+        return;
+    }
+    if (band_) check_(fresh_ ? gdp_build(band_, nullptr) : gdp_generate_dog(band_, nullptr), "GenerateDoG_mpi", band_);
     check_comm_(gdp_comm_gather_bands(comm_, band_, 0, rank_ == 0 ? full_ : nullptr, 0, 0, nullptr), "GenerateDoG_mpi",
                 comm_);
+    fresh_ = false;
+    band_live_ = true;
     if (rank_ == 0) sync_host_();
 }
 

@@ -9,9 +9,11 @@
 // 0..S+1, Gaussian S+2) in GaussPy and print the elapsed seconds like the collector rank does
 // (mpitest.cpp:95-96, :171-172).  The reference's MPI fan-out over S+3 worker ranks is replaced by
 // the GPU; the functions can be called repeatedly (no MPI_Init/MPI_Finalize inside).
-// Note: mpitest.cpp's window centre is float(len-1)/2 (:44); this build uses the serial
-// GuassDePyramid.h centre (float length halved, :107-115) — identical for power-of-two n, which is
-// the only size mpitest.cpp runs (n = 256, :548).
+// Window centre: mpitest.cpp centres on the INTEGER octave length, `l = float(len - 1) / 2.0`
+// (:44, :123), not on GuassDePyramid.h's float-halved length (:107-115); the context uses the same
+// (GDP_CENTRE_INTLEN), so the result equals mpitest.cpp's collector for every n — the two centres
+// agree for power-of-two n (mpitest.cpp runs n = 256, :548) and differ e.g. for n = 100 (pinned
+// against the reference's own runs under mpiexec, tests/golden/mpi_hashes.json).
 #ifndef SIFT_GAUSSDEPYRAMID_HIP_MPITEST_H
 #define SIFT_GAUSSDEPYRAMID_HIP_MPITEST_H
 
@@ -59,6 +61,7 @@ void GaussPyInit(int* data[MAX]) {
             }
         }
         gdp_mpitest_check(gdp_create(&gdp_mpitest_ctx, length, length, S, layer, 1, 0), "GaussPyInit");
+        gdp_mpitest_check(gdp_set_window_centre(gdp_mpitest_ctx, GDP_CENTRE_INTLEN), "GaussPyInit");
     }
     is_initialized = true;
     gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");

@@ -25,6 +25,12 @@
 #ifndef SIFT_GAUSSDEPYRAMID_HIP_H
 #define SIFT_GAUSSDEPYRAMID_HIP_H
 
+// What a caller of the replaced header gets transitively: GaussDePyramid-MPI.h:8-13 pulls in
+// <iostream>, <chrono>, <math.h> and <sys/time.h>, and main.cpp:62-69 relies on <chrono>.
+#include <math.h>
+#include <sys/time.h>
+
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>

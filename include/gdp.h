@@ -51,7 +51,8 @@ enum {
     GDP_ERR_HIP = 2,      /* a HIP runtime call failed (message in gdp_last_error)   */
     GDP_ERR_STATE = 3,    /* call not valid in the context's current state           */
     GDP_ERR_NOMEM = 4,    /* host or device allocation failed                        */
-    GDP_ERR_NODEV = 5     /* no usable gfx950 device                                 */
+    GDP_ERR_NODEV = 5,    /* no usable gfx950 device                                 */
+    GDP_ERR_INTERNAL = 6  /* unexpected internal failure (a C++ exception stopped at the ABI) */
 };
 
 /* ABI version of this header; gdp_abi_version() returns the library's. */
@@ -186,6 +187,28 @@ int gdp_checksum(gdp_ctx* ctx, int b, uint64_t* out);
  * copied to host (cols_o or rows-of-whole-image_o floats).  Lets tests pin the host taps against
  * the reference's own (tests/golden/taps.npz). */
 int gdp_get_taps(gdp_ctx* ctx, int axis, int octave, int scale, float* host);
+
+/* ---- window centre ------------------------------------------------------------------------
+ * Where the 1-D window of octave o is centred.  GDP_CENTRE_SERIAL (default): c = (len_f - 1) / 2
+ * with len_f the FLOAT axis length halved o times (GuassDePyramid.h:107-115, also
+ * GaussPyramid_mpi::GaussFilter, GaussDePyramid-MPI.h:134-143).  GDP_CENTRE_INTLEN:
+ * c = float(len_o - 1) / 2 with the INTEGER length len_o = n >> o, what the multi-process variants
+ * compute (GaussPyramid_mpi::GenerateDoG_mpi, GaussDePyramid-MPI.h:273; mpitest.cpp:44,123).  The
+ * two agree bit for bit whenever every octave's float length is whole (n a multiple of
+ * 2^(octaves-1)); they differ for e.g. n = 100 from octave 3 on.  Re-uploads the tap tables
+ * (drains the device first).  Pure layout of the taps: kernels and bytes are unchanged. */
+enum { GDP_CENTRE_SERIAL = 0, GDP_CENTRE_INTLEN = 1 };
+int gdp_set_window_centre(gdp_ctx* ctx, int mode);
+int gdp_get_window_centre(const gdp_ctx* ctx);
+
+/* ---- band state ----------------------------------------------------------------------------
+ * Copy the band's rows of every level of `full` (a whole-image context of the same H, W, S and
+ * octaves) image `full_image` into band context `band` image `band_image`: the band then holds
+ * exactly its rows of the whole pyramid's CURRENT contents, so an in-place call on the band
+ * (gdp_generate_dog, gdp_gauss_octave, ...) continues where the whole image left off (the
+ * operation is pointwise).  Device-to-device, ordered on `stream` (NULL = the band's stream),
+ * blocking.  Used by the MPI drop-in to re-enter GenerateDoG_mpi after single-process calls. */
+int gdp_copy_band(gdp_ctx* band, int band_image, const gdp_ctx* full, int full_image, void* stream);
 
 /* ---- tuning (performance only; results are bit-identical for every setting) --------------- */
 enum {

@@ -28,6 +28,26 @@ typedef struct gdp_comm gdp_comm;
  * multiples of 2^(max(octaves,5)-1), the last band ends at H (what gdp_create_band accepts). */
 int gdp_band_rows(int height, int nranks, int rank, int octaves, int* row_begin, int* row_end);
 
+/* One point-to-point transfer of the collector's schedule: `rows` x `cols` floats of level
+ * (octave, scale).  SEND: this rank's whole band level to `peer` (the root); RECV: the root takes
+ * sender `peer`'s band level into the whole image's level at row `first_row`; COPY: the root's own
+ * band, device to device, to row `first_row`.  For SEND `first_row` is the band's first row of the
+ * level in the whole image (where the root will put it). */
+enum { GDP_XFER_SEND = 0, GDP_XFER_RECV = 1, GDP_XFER_COPY = 2 };
+typedef struct gdp_transfer {
+    int kind, peer, octave, scale, first_row, rows, cols;
+} gdp_transfer;
+
+/* The transfer schedule gdp_comm_gather_bands executes on rank `rank` of `nranks` (pure host
+ * arithmetic, no device): the sends of a non-root rank in issue order, or the root's receives
+ * (rank-major, then octave, then scale: RCCL matches the sends and receives of one peer pair in
+ * order) followed by its local copies.  Levels with no rows of a band are skipped.  Writes up to
+ * `capacity` records to `out` (may be NULL with capacity 0) and the total count to `*count`;
+ * GDP_ERR_ARG if the schedule does not fit (call again with a larger buffer).  The RCCL
+ * counterpart of the reference's per-row MPI_Send/MPI_Recv loops (GaussDePyramid-MPI.h:285,298). */
+int gdp_comm_plan(int height, int width, int S, int octaves, int nranks, int rank, int root, gdp_transfer* out,
+                  int capacity, int* count);
+
 int gdp_comm_unique_id(unsigned char id[GDP_COMM_ID_BYTES]);
 int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int nranks, int rank, int device);
 void gdp_comm_destroy(gdp_comm* comm);

@@ -59,17 +59,26 @@ size_t gdo_pyramid_floats(int H, int W, int S, int O) { return gdo_level_offset(
  * In C++ `exp(float)`/`sqrt(float)` are the float overloads, i.e. glibc expf/sqrtf; the
  * expression below has the same operand types and evaluation order.  Returns MyLen.
  */
-int gdo_taps(int length, int octave, int scale, float* out) {
+int gdo_taps_centre(int length, int octave, int scale, float* out, int centre_mode) {
     float len = (float)length;
     for (int t = octave; t != 0; --t) len /= 2; /* :109-112 */
     int my_len = (int)len;                      /* :114 */
-    len = (len - 1) / 2;                        /* :115 */
+    if (centre_mode == 1)
+        /* The multi-process variants centre on the INTEGER length: `len /= 2` on an int
+         * (GaussDePyramid-MPI.h:289, mpitest.cpp:62,139) and `l = float(len - 1) / 2.0`
+         * (GaussDePyramid-MPI.h:273, mpitest.cpp:44,123); the tap expression is the same
+         * (GaussDePyramid-MPI.h:278,283; mpitest.cpp:50,56). */
+        len = (float)((double)(float)(my_len - 1) / 2.0);
+    else
+        len = (len - 1) / 2;                    /* :115 */
     float sig = kSigma / (scale + 1);           /* :118 */
     for (int i = 0; i < my_len; ++i) {          /* :119-121 */
         out[i] = expf(-(i - len) * (i - len) / (2 * sig * sig)) / (sig * sqrtf(2 * kPI));
     }
     return my_len;
 }
+
+int gdo_taps(int length, int octave, int scale, float* out) { return gdo_taps_centre(length, octave, scale, out, 0); }
 
 /*
  * Closed form of GaussPyInit + GenerateDoG (GuassDePyramid.h:60-87, 106-149) for the first O
@@ -81,7 +90,8 @@ int gdo_taps(int length, int octave, int scale, float* out) {
  * img has a row pitch of `pitch` int32 elements.  `taps` is scratch of >= 2*(S+3)*max(H,W)
  * floats.
  */
-void gdo_build(const int32_t* img, int H, int W, long pitch, int S, int O, float* out, float* taps) {
+void gdo_build_centre(const int32_t* img, int H, int W, long pitch, int S, int O, float* out, float* taps,
+                      int centre_mode) {
     const int L = S + 3;
     const int mx = H > W ? H : W;
     float* fc = taps;                  /* [L][mx] column-index taps (from W) */
@@ -89,8 +99,8 @@ void gdo_build(const int32_t* img, int H, int W, long pitch, int S, int O, float
     for (int o = 0; o < O; ++o) {
         const int Ho = H >> o, Wo = W >> o;
         for (int s = 0; s < L; ++s) {
-            gdo_taps(W, o, s, fc + (size_t)s * mx);
-            gdo_taps(H, o, s, fr + (size_t)s * mx);
+            gdo_taps_centre(W, o, s, fc + (size_t)s * mx, centre_mode);
+            gdo_taps_centre(H, o, s, fr + (size_t)s * mx, centre_mode);
         }
         float* lev[64];
         for (int s = 0; s < L; ++s) lev[s] = out + gdo_level_offset(H, W, S, o, s);
@@ -109,6 +119,11 @@ void gdo_build(const int32_t* img, int H, int W, long pitch, int S, int O, float
             }
         }
     }
+}
+
+/* GuassDePyramid.h's closed form (serial window centre). */
+void gdo_build(const int32_t* img, int H, int W, long pitch, int S, int O, float* out, float* taps) {
+    gdo_build_centre(img, H, W, pitch, S, O, out, taps, 0);
 }
 
 /*
@@ -153,20 +168,24 @@ void gdo_init(const int32_t* img, int H, int W, long pitch, int S, int O, float*
 }
 
 /* GaussFilter(o) in place (GuassDePyramid.h:106-134): row pass then column pass, per scale. */
-void gdo_gauss_octave(float* pyr, int H, int W, int S, int o, float* taps) {
+void gdo_gauss_octave_centre(float* pyr, int H, int W, int S, int o, float* taps, int centre_mode) {
     const int Ho = H >> o, Wo = W >> o;
     const int mx = H > W ? H : W;
     float* fc = taps;
     float* fr = taps + mx;
     for (int s = 0; s < S + 3; ++s) {
-        gdo_taps(W, o, s, fc);
-        gdo_taps(H, o, s, fr);
+        gdo_taps_centre(W, o, s, fc, centre_mode);
+        gdo_taps_centre(H, o, s, fr, centre_mode);
         float* lev = pyr + gdo_level_offset(H, W, S, o, s);
         for (int j = 0; j < Ho; ++j) /* :122-126 row pass, column-index tap */
             for (int k = 0; k < Wo; ++k) lev[(size_t)j * Wo + k] *= fc[k];
         for (int j = 0; j < Wo; ++j) /* :127-131 column pass, row-index tap (column-major walk) */
             for (int k = 0; k < Ho; ++k) lev[(size_t)k * Wo + j] *= fr[k];
     }
+}
+
+void gdo_gauss_octave(float* pyr, int H, int W, int S, int o, float* taps) {
+    gdo_gauss_octave_centre(pyr, H, W, S, o, taps, 0);
 }
 
 /* DoG subtraction of one octave in place (GuassDePyramid.h:140-146), s ascending. */
@@ -183,11 +202,15 @@ void gdo_dog_octave(float* pyr, int H, int W, int S, int o) {
  * reference's operation order.  Called on a fresh GaussPyInit it equals gdo_build; called again
  * it re-filters the DoG levels, which is what the reference's repeated-call timing loop does
  * (main.cpp:66-73). */
-void gdo_generate_dog(float* pyr, int H, int W, int S, int O, float* taps) {
+void gdo_generate_dog_centre(float* pyr, int H, int W, int S, int O, float* taps, int centre_mode) {
     for (int o = 0; o < O; ++o) {
-        gdo_gauss_octave(pyr, H, W, S, o, taps);
+        gdo_gauss_octave_centre(pyr, H, W, S, o, taps, centre_mode);
         gdo_dog_octave(pyr, H, W, S, o);
     }
+}
+
+void gdo_generate_dog(float* pyr, int H, int W, int S, int O, float* taps) {
+    gdo_generate_dog_centre(pyr, H, W, S, O, taps, 0);
 }
 
 /* GaussPyramid_a512omp::GenerateDoG_nomp_dynamic (GaussDePyramid-AVX512xOpenMP.h:240-364)

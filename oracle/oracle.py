@@ -40,6 +40,9 @@ def lib():
         L.gdo_pyramid_floats.argtypes, L.gdo_pyramid_floats.restype = [i, i, i, i], sz
         L.gdo_taps.argtypes, L.gdo_taps.restype = [i, i, i, p], i
         L.gdo_build.argtypes, L.gdo_build.restype = [p, i, i, lng, i, i, p, p], None
+        L.gdo_taps_centre.argtypes, L.gdo_taps_centre.restype = [i, i, i, p, i], i
+        L.gdo_generate_dog_centre.argtypes, L.gdo_generate_dog_centre.restype = [p, i, i, i, i, p, i], None
+        L.gdo_build_centre.argtypes, L.gdo_build_centre.restype = [p, i, i, lng, i, i, p, p, i], None
         L.gdo_init.argtypes, L.gdo_init.restype = [p, i, i, lng, i, i, p], None
         L.gdo_gauss_octave.argtypes, L.gdo_gauss_octave.restype = [p, i, i, i, i, p], None
         L.gdo_dog_octave.argtypes, L.gdo_dog_octave.restype = [p, i, i, i, i], None
@@ -85,9 +88,12 @@ def levels(pyr, H, W, S, O):
     return out
 
 
-def taps(length, o, s):
+CENTRES = {"serial": 0, "intlen": 1}  # GuassDePyramid.h:107-115 / GaussDePyramid-MPI.h:273
+
+
+def taps(length, o, s, centre="serial"):
     out = np.zeros(max(length, 1), np.float32)
-    m = lib().gdo_taps(int(length), int(o), int(s), _ptr(out))
+    m = lib().gdo_taps_centre(int(length), int(o), int(s), _ptr(out), CENTRES[centre])
     return out[:m].copy()
 
 
@@ -95,13 +101,15 @@ def _scratch(H, W, S):
     return np.zeros(2 * (S + 3) * max(H, W, 1), np.float32)
 
 
-def build_pyramid(img, S, O=None):
-    """Closed-form GaussPyInit + GenerateDoG for the first O octaves; packed layout."""
+def build_pyramid(img, S, O=None, centre="serial"):
+    """Closed-form GaussPyInit + GenerateDoG for the first O octaves; packed layout.  centre
+    "intlen" restates the multi-process variants (GaussDePyramid-MPI.h:265-335, mpitest.cpp:35-189),
+    whose window centre uses the integer octave length."""
     img = np.ascontiguousarray(img, dtype=np.int32)
     H, W = img.shape
     O = default_octaves(H, W) if O is None else O
     out = np.empty(pyramid_floats(H, W, S, O), np.float32)
-    lib().gdo_build(_ptr(img), H, W, W, S, O, _ptr(out), _ptr(_scratch(H, W, S)))
+    lib().gdo_build_centre(_ptr(img), H, W, W, S, O, _ptr(out), _ptr(_scratch(H, W, S)), CENTRES[centre])
     return out
 
 
@@ -114,10 +122,11 @@ def init_pyramid(img, S, O=None):
     return out
 
 
-def generate_dog(pyr, H, W, S, O):
-    """In-place GenerateDoG on the current contents (reference operation order)."""
+def generate_dog(pyr, H, W, S, O, centre="serial"):
+    """In-place GenerateDoG on the current contents (reference operation order); centre "intlen"
+    for the multi-process variants' GenerateDoG_mpi (GaussDePyramid-MPI.h:271-318)."""
     assert pyr.dtype == np.float32 and pyr.flags.c_contiguous
-    lib().gdo_generate_dog(_ptr(pyr), H, W, S, O, _ptr(_scratch(H, W, S)))
+    lib().gdo_generate_dog_centre(_ptr(pyr), H, W, S, O, _ptr(_scratch(H, W, S)), CENTRES[centre])
     return pyr
 
 

@@ -18,7 +18,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GDP_LIBRARY", os.path.join(PKG_DIR, "lib", "libgdp.so"))
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "gdp.h")
 
-GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV = range(6)
+GDP_OK, GDP_ERR_ARG, GDP_ERR_HIP, GDP_ERR_STATE, GDP_ERR_NOMEM, GDP_ERR_NODEV, GDP_ERR_INTERNAL = range(7)
+GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN = 0, 1
 GDP_INPUT_I32, GDP_INPUT_U8 = 0, 1
 GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT, GDP_TUNE_TILE_ORDER = 1, 2, 3, 4, 5
 GDP_TUNE_INPLACE_SUB, GDP_TUNE_WINDOW_SUB, GDP_TUNE_CONV_KERNEL, GDP_TUNE_CONV_ROWS = 6, 7, 8, 9
@@ -77,6 +78,9 @@ SIGNATURES = {
     "gdp_level_offset": (_c_size, [_p, _c_int, _c_int, _c_int]),
     "gdp_checksum": (_c_int, [_p, _c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "gdp_get_taps": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_set_window_centre": (_c_int, [_p, _c_int]),
+    "gdp_get_window_centre": (_c_int, [_p]),
+    "gdp_copy_band": (_c_int, [_p, _c_int, _p, _c_int, _p]),
     "gdp_sync": (_c_int, [_p]),
     "gdp_stream": (_p, [_p]),
     "gdp_last_error": (ctypes.c_char_p, [_p]),

@@ -51,12 +51,18 @@ const float kSigma = 2.0f;
 const float kPI = 3.1414926f;
 
 // GuassDePyramid.h:107-121, evaluated on the host in the reference's float expression order:
-// the window centre is the FLOAT length halved o times, minus 1, over 2 (:107-115).
-int host_taps(int length, int octave, int scale, float* out) {
+// the window centre is the FLOAT length halved o times, minus 1, over 2 (:107-115).  With
+// GDP_CENTRE_INTLEN the centre is float(len_o - 1) / 2 of the INTEGER length len_o = length >> o,
+// as the multi-process variants compute it (GaussDePyramid-MPI.h:273, mpitest.cpp:44,123); their
+// tap expression is otherwise the same (GaussDePyramid-MPI.h:278,283).
+int host_taps(int length, int octave, int scale, float* out, int centre_mode) {
     float len = (float)length;
     for (int t = octave; t != 0; --t) len /= 2;
     const int my_len = (int)len;
-    len = (len - 1) / 2;
+    if (centre_mode == GDP_CENTRE_INTLEN)
+        len = (float)((double)(my_len - 1) / 2.0);  // l = float(len - 1) / 2.0
+    else
+        len = (len - 1) / 2;
     const float sig = kSigma / (scale + 1);
     for (int i = 0; i < my_len; ++i) out[i] = expf(-(i - len) * (i - len) / (2 * sig * sig)) / (sig * sqrtf(2 * kPI));
     return my_len;
@@ -90,6 +96,7 @@ struct gdp_ctx {
     int conv_order = 5;           // GDP_TUNE_CONV_ORDER (default set per geometry in gdp_create): bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
                                   // bit 2 input-row-interleaved octaves (conv_sweep_perm)
     int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
+    int centre_mode = GDP_CENTRE_SERIAL; // gdp_set_window_centre
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
     int* d_cradius = nullptr;     // convolution-mode radius per scale
     unsigned* d_conv_perm = nullptr; // conv sweep block order for GDP_TUNE_CONV_ORDER bit 2 (per image)
@@ -230,6 +237,19 @@ int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     }
 }
 
+// Column taps of every (o, s) from W, row taps from H (aliased for square images), in the
+// context's window-centre mode (host memory only).
+void fill_host_taps(gdp_ctx* c) {
+    const Geom& g = c->geom;
+    for (int o = 0; o < g.O; ++o) {
+        const OctGeom& og = g.oct[o];
+        for (int s = 0; s < g.L; ++s) {
+            host_taps(g.W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride, c->centre_mode);
+            host_taps(g.H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride, c->centre_mode);
+        }
+    }
+}
+
 bool valid_level(const gdp_ctx* c, int b, int o, int s) {
     return c && b >= 0 && b < c->geom.batch && o >= 0 && o < c->geom.O && s >= 0 && s < c->geom.L;
 }
@@ -311,16 +331,36 @@ hipError_t launch_conv_sweep_l(gdp_ctx* c, unsigned grid, hipStream_t st) {
     return c->conv_rows == 32 ? launch_conv_sweep_t<L, 32>(c, grid, st) : launch_conv_sweep_t<L, 16>(c, grid, st);
 }
 
+// ---- no C++ exception crosses the C ABI --------------------------------------------------------
+// Every int-returning export is a function-try-block ending in GDP_ABI_CATCH(ctx): std::bad_alloc
+// becomes GDP_ERR_NOMEM, anything else GDP_ERR_INTERNAL, with the text in gdp_last_error(ctx)
+// (ctx NULL: the thread's create error).  The exports that return pointers / sizes / void do not
+// allocate.
+static int abi_exception(const gdp_ctx* c, int code, const char* what) noexcept {
+    try {
+        if (c)
+            const_cast<gdp_ctx*>(c)->err = what;
+        else
+            g_create_error = what;
+    } catch (...) {
+    }
+    return code;
+}
+#define GDP_ABI_CATCH(ctx)                                                                                   \
+    catch (const std::bad_alloc&) { return abi_exception((ctx), GDP_ERR_NOMEM, "host allocation failed (std::bad_alloc)"); } \
+    catch (const std::exception& e_) { return abi_exception((ctx), GDP_ERR_INTERNAL, e_.what()); }         \
+    catch (...) { return abi_exception((ctx), GDP_ERR_INTERNAL, "unknown C++ exception"); }
+
 extern "C" {
 
 int gdp_abi_version(void) { return GDP_ABI_VERSION; }
 
 int gdp_octaves_for(int n) { return octaves_for(n); }
 
-int gdp_device_count(void) {
+int gdp_device_count(void) try {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
-}
+} GDP_ABI_CATCH(nullptr)
 
 const char* gdp_status_string(int s) {
     switch (s) {
@@ -330,13 +370,14 @@ const char* gdp_status_string(int s) {
         case GDP_ERR_STATE: return "invalid state";
         case GDP_ERR_NOMEM: return "out of memory";
         case GDP_ERR_NODEV: return "no gfx950 device";
+        case GDP_ERR_INTERNAL: return "internal error";
         default: return "unknown status";
     }
 }
 
 const char* gdp_last_error(const gdp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
-int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int row_begin, int row_end, int device) {
+int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int row_begin, int row_end, int device) try {
     if (!out) return GDP_ERR_ARG;
     *out = nullptr;
     auto fail = [](int code, const std::string& m) {
@@ -355,16 +396,17 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         (row_end != H && row_end % align != 0))
         return fail(GDP_ERR_ARG, "gdp_create_band: rows [" + std::to_string(row_begin) + ", " +
                                      std::to_string(row_end) + ") must be multiples of " + std::to_string(align));
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GDP_ERR_NODEV, "no HIP device visible");
-    if (device < 0 || device >= ndev) return fail(GDP_ERR_ARG, "device index out of range");
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail(GDP_ERR_NODEV, "hipGetDeviceProperties failed");
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail(GDP_ERR_NODEV, std::string("libgdp is built for gfx950, device is ") + prop.gcnArchName);
-
+    // Host planning first (geometry, tap tables: pure host work, no device needed), then the
+    // device probe and the allocations.  Anything that throws past this point (std::bad_alloc of
+    // the tap table, ...) frees the half-built context and is turned into a status by the
+    // function-try-block below: no exception crosses the C ABI.
     gdp_ctx* c = new (std::nothrow) gdp_ctx();
     if (!c) return fail(GDP_ERR_NOMEM, "host allocation failed");
+    auto drop = [&c]() {  // free the half-built context exactly once
+        gdp_destroy(c);
+        c = nullptr;
+    };
+    try {
     c->device = device;
     c->variant = default_variant(W, (long long)(row_end - row_begin) * W, batch);
     // Convolution-extension block order (tools/tune.py --op conv, cold buffers): batches 5 (XCD-
@@ -375,8 +417,6 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         const long long px = (long long)(row_end - row_begin) * W;
         c->conv_order = batch > 1 ? 5 : (px >= (1ll << 26) ? 4 : 0);
     }
-    c->cus = std::max(1, prop.multiProcessorCount);
-    c->blocks_max = c->cus * 8;
     Geom& g = c->geom;
     g.H = H;
     g.W = W;
@@ -439,7 +479,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     const long long min_tiles = (long long)((g.in_rows + kTileRows - 1) / kTileRows) * ((W + 63) / 64) * batch;
     if (tap_off > (1ll << 31) || min_tiles + tail_units >= (1ll << 31) || tail_per_img * batch >= (1ll << 31) ||
         grp >= (1ll << 31)) {
-        delete c;
+        drop();
         return fail(GDP_ERR_ARG, "image/batch too large for one context (split the batch)");
     }
     g.tail_groups_per_img = (unsigned)tail_per_img;
@@ -451,17 +491,32 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     retile(c, kVariants[c->variant].tile_cols, kVariants[c->variant].tile_rows);
     conv_sweep_geom(c);
     c->h_taps.assign((size_t)tap_off, 0.0f);
-    for (int o = 0; o < O; ++o) {
-        const OctGeom& og = g.oct[o];
-        for (int s = 0; s < g.L; ++s) {
-            host_taps(W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride);
-            host_taps(H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride);
-        }
+    fill_host_taps(c);
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        drop();
+        return fail(GDP_ERR_NODEV, "no HIP device visible");
     }
+    hipDeviceProp_t prop;
+    if (device < 0 || device >= ndev) {
+        drop();
+        return fail(GDP_ERR_ARG, "device index out of range");
+    }
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        drop();
+        return fail(GDP_ERR_NODEV, "hipGetDeviceProperties failed");
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        drop();
+        return fail(GDP_ERR_NODEV, std::string("libgdp is built for gfx950, device is ") + prop.gcnArchName);
+    }
+    c->cus = std::max(1, prop.multiProcessorCount);
+    c->blocks_max = c->cus * 8;
 
     auto hip_fail = [&](hipError_t e, const char* what) {
         std::string m = std::string(what) + ": " + hipGetErrorString(e);
-        gdp_destroy(c);
+        drop();
         return fail(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, m);
     };
     hipError_t e;
@@ -482,16 +537,20 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     if ((e = hipMemset(c->d_in_own, 0, (size_t)g.in_img_stride * batch * 4)) != hipSuccess) return hip_fail(e, "hipMemset");
     if (upload_geom(c) != GDP_OK) {
         std::string m = c->err;
-        gdp_destroy(c);
+        drop();
         return fail(GDP_ERR_HIP, m);
     }
     *out = c;
     return GDP_OK;
-}
+    } catch (...) {
+        drop();  // safe on a half-built context (null members are skipped)
+        throw;
+    }
+} GDP_ABI_CATCH(nullptr)
 
-int gdp_create(gdp_ctx** out, int H, int W, int S, int O, int batch, int device) {
+int gdp_create(gdp_ctx** out, int H, int W, int S, int O, int batch, int device) try {
     return gdp_create_band(out, H, W, S, O, batch, 0, H, device);
-}
+} GDP_ABI_CATCH(nullptr)
 
 void gdp_destroy(gdp_ctx* c) {
     if (!c) return;
@@ -512,7 +571,7 @@ void gdp_destroy(gdp_ctx* c) {
     delete c;
 }
 
-int gdp_get_geometry(const gdp_ctx* c, int* H, int* W, int* S, int* O, int* batch) {
+int gdp_get_geometry(const gdp_ctx* c, int* H, int* W, int* S, int* O, int* batch) try {
     if (!c) return GDP_ERR_ARG;
     if (H) *H = c->geom.H;
     if (W) *W = c->geom.W;
@@ -520,15 +579,15 @@ int gdp_get_geometry(const gdp_ctx* c, int* H, int* W, int* S, int* O, int* batc
     if (O) *O = c->geom.O;
     if (batch) *batch = c->geom.batch;
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_level_dims(const gdp_ctx* c, int o, int* rows, int* cols, int* first_row) {
+int gdp_level_dims(const gdp_ctx* c, int o, int* rows, int* cols, int* first_row) try {
     if (!c || o < 0 || o >= c->geom.O) return GDP_ERR_ARG;
     if (rows) *rows = c->geom.oct[o].rows;
     if (cols) *cols = c->geom.oct[o].cols;
     if (first_row) *first_row = c->geom.oct[o].row0;
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
 size_t gdp_pyramid_bytes(const gdp_ctx* c) { return c ? (size_t)c->geom.pyr_stride * c->geom.batch * 4 : 0; }
 
@@ -579,18 +638,18 @@ int bind_input(gdp_ctx* c, const void* base, size_t pitch, size_t image_stride, 
 }
 }  // namespace
 
-int gdp_set_input_host(gdp_ctx* c, int b, const int32_t* base, size_t pitch, void* stream) {
+int gdp_set_input_host(gdp_ctx* c, int b, const int32_t* base, size_t pitch, void* stream) try {
     return upload_input(c, b, base, pitch, GDP_INPUT_I32, stream, "gdp_set_input_host");
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_set_input_host_u8(gdp_ctx* c, int b, const uint8_t* base, size_t pitch, void* stream) {
+int gdp_set_input_host_u8(gdp_ctx* c, int b, const uint8_t* base, size_t pitch, void* stream) try {
     return upload_input(c, b, base, pitch, GDP_INPUT_U8, stream, "gdp_set_input_host_u8");
-}
+} GDP_ABI_CATCH(c)
 
 static int ensure_stage(gdp_ctx* c, size_t floats);
 static void parallel_rows(size_t nrows, size_t floats, int threads, const std::function<void(size_t, size_t)>& fn);
 
-int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stream) {
+int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stream) try {
     if (!c || !rows || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_set_input_rows: bad argument") : GDP_ERR_ARG;
     if (c->d_in != c->d_in_own) return c->status(GDP_ERR_STATE, "input is bound to caller device memory");
     if (c->geom.in_fmt != GDP_INPUT_I32)
@@ -620,17 +679,17 @@ int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stre
     }
     GDP_HIP(c, hipStreamSynchronize(st));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_set_input_device(gdp_ctx* c, const int32_t* base, size_t pitch, size_t image_stride) {
+int gdp_set_input_device(gdp_ctx* c, const int32_t* base, size_t pitch, size_t image_stride) try {
     return bind_input(c, base, pitch, image_stride, GDP_INPUT_I32, "gdp_set_input_device");
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_set_input_device_u8(gdp_ctx* c, const uint8_t* base, size_t pitch, size_t image_stride) {
+int gdp_set_input_device_u8(gdp_ctx* c, const uint8_t* base, size_t pitch, size_t image_stride) try {
     return bind_input(c, base, pitch, image_stride, GDP_INPUT_U8, "gdp_set_input_device_u8");
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_set_input_format(gdp_ctx* c, int fmt) {
+int gdp_set_input_format(gdp_ctx* c, int fmt) try {
     if (!c || (fmt != GDP_INPUT_I32 && fmt != GDP_INPUT_U8)) return c ? c->status(GDP_ERR_ARG, "unknown input format") : GDP_ERR_ARG;
     if (fmt == c->geom.in_fmt) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
@@ -644,11 +703,11 @@ int gdp_set_input_format(gdp_ctx* c, int fmt) {
     c->d_in_own = fresh;
     c->geom.in_fmt = fmt;
     return bind_input(c, nullptr, 0, 0, fmt, "gdp_set_input_format");
-}
+} GDP_ABI_CATCH(c)
 
 int gdp_get_input_format(const gdp_ctx* c) { return c ? c->geom.in_fmt : -1; }
 
-int gdp_fill_synthetic(gdp_ctx* c, uint32_t seed, long first_image, void* stream) {
+int gdp_fill_synthetic(gdp_ctx* c, uint32_t seed, long first_image, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     const long long total = (long long)c->geom.in_rows * c->geom.W * c->geom.batch;
@@ -659,24 +718,24 @@ int gdp_fill_synthetic(gdp_ctx* c, uint32_t seed, long first_image, void* stream
                        seed, (long long)first_image);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_build(gdp_ctx* c, void* stream) {
+int gdp_build(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_build(c, c->pick(stream));
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_conv_taps(int S, int scale, float* taps, int* radius) {
+int gdp_conv_taps(int S, int scale, float* taps, int* radius) try {
     if (S < 0 || scale < 0 || scale >= S + 3 || !taps || !radius) return GDP_ERR_ARG;
     const int R = conv_radius_of(scale); // ceil(3 sigma), sigma = 2 / (scale + 1), at most kCvR
     const ConvTaps k = conv_taps_of(scale);
     for (int j = 0; j < kCvMaxTaps; ++j) taps[j] = j <= 2 * R ? k.k[j < R ? R - j : j - R] : 0.0f;
     *radius = R;
     return GDP_OK;
-}
+} GDP_ABI_CATCH(nullptr)
 
-int gdp_build_gaussian(gdp_ctx* c, void* stream) {
+int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     const Geom& g = c->geom;
     if (g.in_row0 != 0 || g.in_rows != g.H)
@@ -718,37 +777,37 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) {
                        c->d_geom, c->d_in, c->d_out, c->d_ctaps, c->d_cradius, sweep ? 1 : 0);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_init(gdp_ctx* c, void* stream) {
+int gdp_init(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<4>(c, 0, c->geom.O, c->pick(stream));
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_gauss_octave(gdp_ctx* c, int o, void* stream) {
+int gdp_gauss_octave(gdp_ctx* c, int o, void* stream) try {
     if (!c || o < 0 || o >= c->geom.O) return c ? c->status(GDP_ERR_ARG, "octave out of range") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<1>(c, o, o + 1, c->pick(stream));
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_gauss_range(gdp_ctx* c, int ob, int oe, void* stream) {
+int gdp_gauss_range(gdp_ctx* c, int ob, int oe, void* stream) try {
     if (!c || ob < 0 || oe > c->geom.O || ob >= oe) return c ? c->status(GDP_ERR_ARG, "octave range invalid") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<1>(c, ob, oe, c->pick(stream));
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_dog_octave(gdp_ctx* c, int o, void* stream) {
+int gdp_dog_octave(gdp_ctx* c, int o, void* stream) try {
     if (!c || o < 0 || o >= c->geom.O) return c ? c->status(GDP_ERR_ARG, "octave out of range") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<2>(c, o, o + 1, c->pick(stream));
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_generate_dog(gdp_ctx* c, void* stream) {
+int gdp_generate_dog(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<3>(c, 0, c->geom.O, c->pick(stream));
-}
+} GDP_ABI_CATCH(c)
 
 const float* gdp_device_level(const gdp_ctx* c, int b, int o, int s) {
     if (!valid_level(c, b, o, s)) return nullptr;
@@ -756,7 +815,7 @@ const float* gdp_device_level(const gdp_ctx* c, int b, int o, int s) {
     return c->d_out + (size_t)b * c->geom.pyr_stride + og.lev_off + (size_t)s * og.lev_stride;
 }
 
-int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) {
+int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) try {
     if (!valid_level(c, b, o, s) || !host) return c ? c->status(GDP_ERR_ARG, "gdp_download_level: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     const OctGeom& og = c->geom.oct[o];
@@ -764,7 +823,7 @@ int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) {
                               c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
 // Row-pointer downloads (the drop-in class's float**** mirror): device levels -> pinned staging ->
 // the caller's rows.  The pinned buffer is split in two halves: batch k's D2H copies go into half
@@ -875,15 +934,15 @@ static int stage_download(gdp_ctx* c, const std::vector<StagePiece>& pieces) {
     return GDP_OK;
 }
 
-int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows) {
+int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows) try {
     if (!valid_level(c, b, o, s) || !rows) return c ? c->status(GDP_ERR_ARG, "gdp_download_level_rows: bad argument") : GDP_ERR_ARG;
     const OctGeom& og = c->geom.oct[o];
     if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
     return stage_download(c, {{gdp_device_level(c, b, o, s), (size_t)og.cols, (size_t)og.rows, rows, 0}});
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py) {
+int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py) try {
     if (!c || !py || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid_rows: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
@@ -896,9 +955,9 @@ int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py)
             pieces.push_back({gdp_device_level(c, b, o, s), (size_t)og.cols, (size_t)og.rows, py[o][s], 0});
     }
     return stage_download(c, pieces);
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int nrows, float* host) {
+int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int nrows, float* host) try {
     if (!valid_level(c, b, o, s) || !host || first_row < 0 || nrows < 0 || first_row > c->geom.oct[o].rows ||
         nrows > c->geom.oct[o].rows - first_row)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_level_range: bad argument") : GDP_ERR_ARG;
@@ -909,9 +968,9 @@ int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int
                               (size_t)nrows * og.cols * 4, hipMemcpyDeviceToHost, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_download_pyramid(gdp_ctx* c, int b, float* host) {
+int gdp_download_pyramid(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     size_t off = 0;
@@ -923,9 +982,9 @@ int gdp_download_pyramid(gdp_ctx* c, int b, float* host) {
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) {
+int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_upload_pyramid: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     size_t off = 0;
@@ -939,9 +998,9 @@ int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) {
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) {
+int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) try {
     if (!c || !host || o < 0 || o >= c->geom.O || s < 0 || s >= c->geom.L || (axis != 0 && axis != 1))
         return c ? c->status(GDP_ERR_ARG, "gdp_get_taps: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
@@ -951,9 +1010,9 @@ int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) {
     // read back what the device holds, not the host copy: this is what the kernels use
     GDP_HIP(c, hipMemcpy(host, c->d_taps + off, (size_t)n * 4, hipMemcpyDeviceToHost));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_set_output_device(gdp_ctx* c, float* base, size_t bytes) {
+int gdp_set_output_device(gdp_ctx* c, float* base, size_t bytes) try {
     if (!c) return GDP_ERR_ARG;
     if (!base) {
         c->d_out = c->d_out_own;
@@ -965,7 +1024,7 @@ int gdp_set_output_device(gdp_ctx* c, float* base, size_t bytes) {
     GDP_HIP(c, hipDeviceSynchronize());
     c->d_out = base;
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
 size_t gdp_level_offset(const gdp_ctx* c, int b, int o, int s) {
     if (!valid_level(c, b, o, s)) return (size_t)-1;
@@ -973,7 +1032,7 @@ size_t gdp_level_offset(const gdp_ctx* c, int b, int o, int s) {
     return (size_t)b * c->geom.pyr_stride + og.lev_off + (size_t)s * og.lev_stride;
 }
 
-int gdp_checksum(gdp_ctx* c, int b, uint64_t* out) {
+int gdp_checksum(gdp_ctx* c, int b, uint64_t* out) try {
     if (!c || !out || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_checksum: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     GDP_HIP(c, hipMemsetAsync(c->d_sum, 0, sizeof(unsigned long long), c->stream));
@@ -987,18 +1046,54 @@ int gdp_checksum(gdp_ctx* c, int b, uint64_t* out) {
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     *out = v;
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_sync(gdp_ctx* c) {
+int gdp_set_window_centre(gdp_ctx* c, int mode) try {
+    if (!c || (mode != GDP_CENTRE_SERIAL && mode != GDP_CENTRE_INTLEN))
+        return c ? c->status(GDP_ERR_ARG, "gdp_set_window_centre: mode must be GDP_CENTRE_SERIAL or GDP_CENTRE_INTLEN") : GDP_ERR_ARG;
+    if (mode == c->centre_mode) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipDeviceSynchronize());  // no in-flight launch reads a half-written table
+    c->centre_mode = mode;
+    fill_host_taps(c);
+    GDP_HIP(c, hipMemcpy(c->d_taps, c->h_taps.data(), c->h_taps.size() * 4, hipMemcpyHostToDevice));
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+int gdp_get_window_centre(const gdp_ctx* c) { return c ? c->centre_mode : -1; }
+
+int gdp_copy_band(gdp_ctx* band, int bi, const gdp_ctx* full, int fi, void* stream) try {
+    if (!band || !full || bi < 0 || bi >= band->geom.batch || fi < 0 || fi >= full->geom.batch)
+        return band ? band->status(GDP_ERR_ARG, "gdp_copy_band: bad argument") : GDP_ERR_ARG;
+    const Geom &gb = band->geom, &gf = full->geom;
+    if (gb.H != gf.H || gb.W != gf.W || gb.S != gf.S || gb.O != gf.O || gf.in_row0 != 0 || gf.in_rows != gf.H)
+        return band->status(GDP_ERR_ARG, "gdp_copy_band: `full` must be a whole-image context of the same geometry");
+    if (band->device != full->device) return band->status(GDP_ERR_ARG, "gdp_copy_band: contexts on different devices");
+    GDP_HIP(band, hipSetDevice(band->device));
+    GDP_HIP(band, hipStreamSynchronize(full->stream));  // full's own work has landed
+    const hipStream_t st = band->pick(stream);
+    for (int o = 0; o < gb.O; ++o) {
+        const OctGeom& og = gb.oct[o];
+        if ((size_t)og.rows * og.cols == 0) continue;
+        for (int s = 0; s < gb.L; ++s)
+            GDP_HIP(band, hipMemcpyAsync(const_cast<float*>(gdp_device_level(band, bi, o, s)),
+                                         gdp_device_level(full, fi, o, s) + (size_t)og.row0 * og.cols,
+                                         (size_t)og.rows * og.cols * 4, hipMemcpyDeviceToDevice, st));
+    }
+    GDP_HIP(band, hipStreamSynchronize(st));
+    return GDP_OK;
+} GDP_ABI_CATCH(band)
+
+int gdp_sync(gdp_ctx* c) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
 void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* best_order, float* best_ms) {
+int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* best_order, float* best_ms) try {
     // Times every build-kernel variant x tile order on the context's current input (HIP events on
     // `stream`, median of 3 repeats of `iters` launches) and keeps the fastest.  All candidates
     // produce identical bits, so this only ever changes speed.
@@ -1031,9 +1126,9 @@ int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* be
     if (best_order) *best_order = bo;
     if (best_ms) *best_ms = bt / iters;
     return GDP_OK;
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
+int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
     if (!c || !value) return GDP_ERR_ARG;
     switch (key) {
         case GDP_TUNE_NONTEMPORAL: *value = c->nontemporal; return GDP_OK;
@@ -1051,9 +1146,9 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) {
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_set_tuning(gdp_ctx* c, int key, int value) {
+int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
     if (!c) return GDP_ERR_ARG;
     switch (key) {
         case GDP_TUNE_NONTEMPORAL:
@@ -1125,9 +1220,9 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) {
         default:
             return c->status(GDP_ERR_ARG, "unknown tuning key %d", key);
     }
-}
+} GDP_ABI_CATCH(c)
 
-int gdp_time_builds(gdp_ctx* c, int iters, void* stream, float* total_ms) {
+int gdp_time_builds(gdp_ctx* c, int iters, void* stream, float* total_ms) try {
     if (!c || iters <= 0 || !total_ms) return c ? c->status(GDP_ERR_ARG, "gdp_time_builds: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     hipStream_t st = c->pick(stream);
@@ -1143,13 +1238,13 @@ int gdp_time_builds(gdp_ctx* c, int iters, void* stream, float* total_ms) {
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return rc;
-}
+} GDP_ABI_CATCH(c)
 
 #ifdef GDP_TRACE_BLOCKS
 // Diagnostic build only: device buffer of 3 x u64 per block for the next build launches (NULL off).
-int gdp_debug_set_block_trace(void* dev_buf) {
+int gdp_debug_set_block_trace(void* dev_buf) try {
     unsigned long long* p = static_cast<unsigned long long*>(dev_buf);
     return hipMemcpyToSymbol(HIP_SYMBOL(g_block_trace), &p, sizeof p) == hipSuccess ? GDP_OK : GDP_ERR_HIP;
-}
+} GDP_ABI_CATCH(nullptr)
 #endif
 }  // extern "C"

@@ -52,11 +52,49 @@ void band_level(int H, int o, int r0, int r1, int* first, int* rows) {
     const int hi = (r1 == H) ? Hg : std::min(Hg, (r1 + (1 << o) - 1) >> o);
     *rows = std::max(0, hi - *first);
 }
+// The collector's schedule (gdp_comm_plan): a non-root rank sends each non-empty level of its
+// band, octave-major then scale; the root posts, for every other rank in rank order, the matching
+// receives in the same order, then copies its own band's levels.
+std::vector<gdp_transfer> make_plan(int H, int W, int S, int O, int nranks, int rank, int root) {
+    std::vector<gdp_transfer> plan;
+    const int L = S + 3;
+    auto band_levels = [&](int r, int kind, int peer) {
+        int r0 = 0, r1 = 0;
+        gdp_band_rows(H, nranks, r, O, &r0, &r1);
+        if (r1 <= r0) return;
+        for (int o = 0; o < O; ++o) {
+            int first, rows;
+            band_level(H, o, r0, r1, &first, &rows);
+            for (int s = 0; s < L && rows > 0; ++s) plan.push_back({kind, peer, o, s, first, rows, W >> o});
+        }
+    };
+    if (rank != root) {
+        band_levels(rank, GDP_XFER_SEND, root);
+        return plan;
+    }
+    for (int r = 0; r < nranks; ++r)
+        if (r != root) band_levels(r, GDP_XFER_RECV, r);
+    band_levels(root, GDP_XFER_COPY, root);
+    return plan;
+}
+
+int fail_nothrow(gdp_comm* c, int code, const char* m) noexcept {
+    try {
+        return fail(c, code, m);
+    } catch (...) {
+        return code;
+    }
+}
+// no C++ exception crosses the C ABI (std::bad_alloc -> GDP_ERR_NOMEM, others -> GDP_ERR_INTERNAL)
+#define GDP_COMM_CATCH(c)                                                                                  \
+    catch (const std::bad_alloc&) { return fail_nothrow((c), GDP_ERR_NOMEM, "host allocation failed"); }    \
+    catch (const std::exception& e_) { return fail_nothrow((c), GDP_ERR_INTERNAL, e_.what()); }            \
+    catch (...) { return fail_nothrow((c), GDP_ERR_INTERNAL, "unknown C++ exception"); }
 }  // namespace
 
 extern "C" {
 
-int gdp_band_rows(int H, int nranks, int rank, int octaves, int* row_begin, int* row_end) {
+int gdp_band_rows(int H, int nranks, int rank, int octaves, int* row_begin, int* row_end) try {
     if (H <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || octaves <= 0 || !row_begin || !row_end)
         return GDP_ERR_ARG;
     // per = ceil(ceil(H / nranks) / align) * align — distributed.plan_band, same numbers
@@ -66,18 +104,18 @@ int gdp_band_rows(int H, int nranks, int rank, int octaves, int* row_begin, int*
     *row_begin = (int)std::min<long long>(H, (long long)rank * per);
     *row_end = (int)std::min<long long>(H, (long long)(rank + 1) * per);
     return GDP_OK;
-}
+} GDP_COMM_CATCH(nullptr)
 
-int gdp_comm_unique_id(unsigned char id[GDP_COMM_ID_BYTES]) {
+int gdp_comm_unique_id(unsigned char id[GDP_COMM_ID_BYTES]) try {
     static_assert(sizeof(ncclUniqueId) == GDP_COMM_ID_BYTES, "ncclUniqueId size");
     ncclUniqueId u;
     ncclResult_t r = ncclGetUniqueId(&u);
     if (r != ncclSuccess) return fail(nullptr, GDP_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
     std::memcpy(id, &u, sizeof u);
     return GDP_OK;
-}
+} GDP_COMM_CATCH(nullptr)
 
-int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int nranks, int rank, int device) {
+int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int nranks, int rank, int device) try {
     if (!out || !id || nranks <= 0 || rank < 0 || rank >= nranks) return fail(nullptr, GDP_ERR_ARG, "gdp_comm_init: bad argument");
     *out = nullptr;
     gdp_comm* c = new (std::nothrow) gdp_comm();
@@ -99,7 +137,7 @@ int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int
     }
     *out = c;
     return GDP_OK;
-}
+} GDP_COMM_CATCH(nullptr)
 
 void gdp_comm_destroy(gdp_comm* c) {
     if (!c) return;
@@ -111,10 +149,22 @@ int gdp_comm_rank(const gdp_comm* c) { return c ? c->rank : -1; }
 int gdp_comm_size(const gdp_comm* c) { return c ? c->nranks : -1; }
 const char* gdp_comm_last_error(const gdp_comm* c) { return c ? c->err.c_str() : g_comm_error.c_str(); }
 
+int gdp_comm_plan(int H, int W, int S, int O, int nranks, int rank, int root, gdp_transfer* out, int capacity,
+                  int* count) try {
+    if (H <= 0 || W <= 0 || S < 0 || O <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || root < 0 ||
+        root >= nranks || !count || capacity < 0 || (capacity > 0 && !out))
+        return fail(nullptr, GDP_ERR_ARG, "gdp_comm_plan: bad argument");
+    std::vector<gdp_transfer> plan = make_plan(H, W, S, O, nranks, rank, root);
+    *count = (int)plan.size();
+    if ((int)plan.size() > capacity) return fail(nullptr, GDP_ERR_ARG, "gdp_comm_plan: capacity too small");
+    std::copy(plan.begin(), plan.end(), out);
+    return GDP_OK;
+} GDP_COMM_CATCH(nullptr)
+
 int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* full, int full_image, int root,
-                          void* stream) {
+                          void* stream) try {
     // band == NULL: this rank's band is empty (more ranks than aligned row bands); it sends nothing
-    if (!c || root < 0 || root >= c->nranks || (c->rank == root && !full) || (!band && c->rank == root && !full))
+    if (!c || root < 0 || root >= c->nranks || (c->rank == root && !full))
         return fail(c, GDP_ERR_ARG, "gdp_comm_gather_bands: bad argument");
     int H, W, S, O, B;
     if (gdp_get_geometry(band ? band : full, &H, &W, &S, &O, &B) != GDP_OK) {
@@ -131,46 +181,35 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
     GDP_HIPC(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)gdp_stream(band ? band : full);
     if (!band && c->rank != root) return GDP_OK;  // empty band: nothing to send, nothing to receive
-    const int L = S + 3;
-    GDP_NCCL(c, ncclGroupStart());
-    if (c->rank != root) {
-        for (int o = 0; o < O; ++o) {
+    const std::vector<gdp_transfer> plan = make_plan(H, W, S, O, c->nranks, c->rank, root);
+    if (band) {  // the band context must hold exactly the rows the plan sends / copies
+        for (const gdp_transfer& t : plan) {
+            if (t.kind == GDP_XFER_RECV) continue;
             int rows, cols, first;
-            gdp_level_dims(band, o, &rows, &cols, &first);
-            for (int s = 0; s < L && rows > 0; ++s)
-                GDP_NCCL(c, ncclSend(gdp_device_level(band, band_image, o, s), (size_t)rows * cols, ncclFloat, root,
-                                     c->comm, st));
-        }
-    } else {
-        for (int r = 0; r < c->nranks; ++r) {
-            if (r == root) continue;
-            int r0, r1;
-            gdp_band_rows(H, c->nranks, r, O, &r0, &r1);
-            for (int o = 0; o < O; ++o) {
-                int first, rows;
-                band_level(H, o, r0, r1, &first, &rows);
-                const int cols = W >> o;
-                for (int s = 0; s < L && rows > 0; ++s) {
-                    float* dst = const_cast<float*>(gdp_device_level(full, full_image, o, s)) + (size_t)first * cols;
-                    GDP_NCCL(c, ncclRecv(dst, (size_t)rows * cols, ncclFloat, r, c->comm, st));
-                }
-            }
+            gdp_level_dims(band, t.octave, &rows, &cols, &first);
+            if (rows != t.rows || cols != t.cols || first != t.first_row)
+                return fail(c, GDP_ERR_ARG, "band context rows differ from gdp_band_rows' band of this rank");
         }
     }
+    GDP_NCCL(c, ncclGroupStart());
+    for (const gdp_transfer& t : plan) {
+        const size_t n = (size_t)t.rows * t.cols;
+        if (t.kind == GDP_XFER_SEND)
+            GDP_NCCL(c, ncclSend(gdp_device_level(band, band_image, t.octave, t.scale), n, ncclFloat, t.peer, c->comm, st));
+        else if (t.kind == GDP_XFER_RECV)
+            GDP_NCCL(c, ncclRecv(const_cast<float*>(gdp_device_level(full, full_image, t.octave, t.scale)) +
+                                     (size_t)t.first_row * t.cols,
+                                 n, ncclFloat, t.peer, c->comm, st));
+    }
     GDP_NCCL(c, ncclGroupEnd());
-    if (c->rank == root && band) {  // the collector's own band: device-to-device copies
-        for (int o = 0; o < O; ++o) {
-            int rows, cols, first;
-            gdp_level_dims(band, o, &rows, &cols, &first);
-            for (int s = 0; s < L && rows > 0; ++s) {
-                float* dst = const_cast<float*>(gdp_device_level(full, full_image, o, s)) + (size_t)first * cols;
-                GDP_HIPC(c, hipMemcpyAsync(dst, gdp_device_level(band, band_image, o, s), (size_t)rows * cols * 4,
-                                           hipMemcpyDeviceToDevice, st));
-            }
-        }
+    for (const gdp_transfer& t : plan) {  // the collector's own band: device-to-device copies
+        if (t.kind != GDP_XFER_COPY || !band) continue;
+        float* dst = const_cast<float*>(gdp_device_level(full, full_image, t.octave, t.scale)) + (size_t)t.first_row * t.cols;
+        GDP_HIPC(c, hipMemcpyAsync(dst, gdp_device_level(band, band_image, t.octave, t.scale),
+                                   (size_t)t.rows * t.cols * 4, hipMemcpyDeviceToDevice, st));
     }
     GDP_HIPC(c, hipStreamSynchronize(st));
     return GDP_OK;
-}
+} GDP_COMM_CATCH(c)
 
 }  // extern "C"

@@ -152,7 +152,7 @@ def assemble_bands(H, W, S, octaves, world, packed_bands, like=None):
     return full
 
 
-def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None):
+def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None, centre="serial"):
     """Collector semantics of GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335) over RCCL.
 
     Every rank passes the same `img` (the reference also replicates the input on every rank,
@@ -160,6 +160,8 @@ def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None
     GPU; rank 0 gathers the bands and returns the full packed pyramid (torch tensor, on its GPU);
     other ranks return None.  `compute(img_band, r0, r1) -> packed float32 torch tensor` may be
     injected (tests use it to run this logic under gloo on CPU); by default it is the HIP build.
+    `centre="intlen"` reproduces the MPI variant's own window centre (GaussDePyramid-MPI.h:273;
+    differs from the serial header only when n is not a multiple of 2^(octaves-1)).
     """
     import torch
 
@@ -169,7 +171,7 @@ def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None
     r0, r1 = plan_band(n, world, rank, O)
     img = np.asarray(img, dtype=np.int32)[:n, :n]
     if compute is None:
-        compute = _gpu_band_compute(n, n, S, O, device)
+        compute = _gpu_band_compute(n, n, S, O, device, centre)
     band = compute(np.ascontiguousarray(img[r0:r1]), r0, r1)
     if world == 1:
         return assemble_bands(n, n, S, O, 1, [band])
@@ -184,7 +186,7 @@ def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None
     return assemble_bands(n, n, S, O, world, [g[:sizes[r]] for r, g in enumerate(gathered)])
 
 
-def _gpu_band_compute(H, W, S, O, device):
+def _gpu_band_compute(H, W, S, O, device, centre="serial"):
     """Default band compute: a libgdp band context writing straight into a torch tensor."""
     import torch
 
@@ -195,7 +197,8 @@ def _gpu_band_compute(H, W, S, O, device):
     def compute(img_band, r0, r1):
         if r1 <= r0:  # more ranks than aligned bands: this rank holds no rows
             return torch.empty(0, dtype=torch.float32, device=dev)
-        with PyramidContext(H, W, S=S, octaves=O, batch=1, device=dev.index, row_begin=r0, row_end=r1) as ctx:
+        with PyramidContext(H, W, S=S, octaves=O, batch=1, device=dev.index, row_begin=r0, row_end=r1,
+                            centre=centre) as ctx:
             out = torch.empty(ctx.pyramid_bytes() // 4 + 64, dtype=torch.float32, device=dev)
             base = out.data_ptr()
             shift = (-base % 256) // 4  # 256-B aligned view

@@ -68,7 +68,7 @@ class PyramidContext:
     """
 
     def __init__(self, height, width, S=2, octaves=0, batch=1, device=0, row_begin=0, row_end=None,
-                 input_format="i32"):
+                 input_format="i32", centre="serial"):
         L = lib()
         self._ctx = ctypes.c_void_p()
         row_end = height if row_end is None else row_end
@@ -88,6 +88,22 @@ class PyramidContext:
         self.input_format = "i32"
         if input_format != "i32":
             self.set_input_format(input_format)
+        self.centre = "serial"
+        if centre != "serial":
+            self.set_window_centre(centre)
+
+    def set_window_centre(self, mode):
+        """'serial' (GuassDePyramid.h:107-115: the float length halved o times) or 'intlen'
+        (the multi-process variants' integer length, GaussDePyramid-MPI.h:273, mpitest.cpp:44)."""
+        from ._lib import GDP_CENTRE_INTLEN, GDP_CENTRE_SERIAL
+
+        code = {"serial": GDP_CENTRE_SERIAL, "intlen": GDP_CENTRE_INTLEN}[mode]
+        check(lib().gdp_set_window_centre(self._ctx, code), self._ctx)
+        self.centre = mode
+
+    def copy_band_from(self, full, b=0, full_image=0, stream=None):
+        """Load this band context's rows of `full`'s current pyramid (gdp_copy_band)."""
+        check(lib().gdp_copy_band(self._ctx, int(b), full._ctx, int(full_image), _stream_handle(stream)), self._ctx)
 
     def set_input_format(self, fmt):
         """'i32' (the reference's int pixels) or 'u8' (8-bit images, 4x fewer input bytes)."""

@@ -15,9 +15,14 @@ Outputs (all plain data, loadable without pickle):
   taps.npz      the reference's `filter` taps for every (octave, scale) — read from the
                 reference object itself (TapProbe in oracle/ref_harness.cpp)
   checksums.json gdp_checksum values of the reference's output for the bench inputs
+  mpi_hashes.json per-level hashes of the COLLECTOR's pyramid of the reference's multi-process
+                variants — GaussPyramid_mpi::GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335) and
+                mpitest.cpp's GenerateDoG_mpi / GenerateDoG_mpi_omp (:35-189) — run under
+                conda MPICH's mpiexec with S+4 ranks (oracle/_ref/ref_mpi, ref_mpitest)
   meta.json     generator provenance (glibc, g++, input definitions)
 
-Usage:  make -C oracle ref && python tests/golden/gen_golden.py
+Usage:  make -C oracle ref ref-mpi && python tests/golden/gen_golden.py [--only PART,...]
+        PART: hashes, dumps, taps, checksums, mpi (default: all)
 """
 import json
 import os
@@ -32,6 +37,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF_SERIAL = os.path.join(REPO, "oracle", "_ref", "ref_serial")
 REF_AVX512 = os.path.join(REPO, "oracle", "_ref", "ref_avx512")
+REF_MPI = os.path.join(REPO, "oracle", "_ref", "ref_mpi")
+REF_MPITEST = os.path.join(REPO, "oracle", "_ref", "ref_mpitest")
+MPIEXEC = os.environ.get("MPIEXEC", "/opt/conda/bin/mpiexec")
 
 # (n, S, input) cases hashed over EVERY octave the reference builds (floor(log2 n)+1).
 HASH_CASES = [
@@ -55,7 +63,20 @@ WINDOW_CASES = [(512, 2, "lcg:12345"), (4096, 2, "lcg:12345")]
 WINDOW = 96
 # bench inputs (config 2/4 image 0 and 1; config 5 image 0) for gdp_checksum fixtures
 CHECKSUM_CASES = [(4096, 2, "synth:0x5EED:0"), (4096, 2, "synth:0x5EED:1"), (512, 2, "lcg:12345"),
-                  (16384, 2, "synth:0x5EED:0")]
+                  (16384, 2, "synth:0x5EED:0"),
+                  # config 4 (512 x 4096^2, 64 per GPU): rank 0's last image and rank 7's first and
+                  # last (global indices past 2^32 pixels: the counter hash folds the index)
+                  (4096, 2, "synth:0x5EED:63"), (4096, 2, "synth:0x5EED:448"), (4096, 2, "synth:0x5EED:511")]
+# bench.py verifies the first and last image of EVERY rank: config 2 at N <= 8 (image r on rank r)
+# and config 4 at N = 8 (images 64r and 64r + 63)
+CHECKSUM_CASES += [(4096, 2, f"synth:0x5EED:{i}") for i in
+                   list(range(2, 8)) + [x for r in range(1, 7) for x in (64 * r, 64 * r + 63)]]
+# the multi-process variants' collector output: (variant, n, S, input); power-of-two n agree with
+# the serial header, non-power-of-two n use the integer-length window centre (GaussDePyramid-MPI.h:273)
+MPI_CASES = [(v, n, S, inp) for v in ("GaussDePyramid-MPI.h:GenerateDoG_mpi", "mpitest.cpp:GenerateDoG_mpi",
+                                       "mpitest.cpp:GenerateDoG_mpi_omp")
+             for n, S, inp in [(512, 2, "lcg:12345"), (256, 2, "ones"), (256, 2, "lcg:12345"),
+                               (100, 2, "lcg:12345"), (1000, 2, "lcg:12345"), (96, 1, "lcg:7")]]
 TAP_CASES = [(512, 2), (100, 2), (1000, 2), (513, 3), (4096, 2), (1080, 2), (1920, 2), (37, 1)]
 
 
@@ -93,10 +114,82 @@ def key(*parts):
     return "_".join(str(p).replace(":", "-") for p in parts)
 
 
+def gen_checksums():
+    # gdp_checksum values (definition in include/gdp.h) of the reference's output for the bench's
+    # own input images, over the first 5 octaves (bench configs) and over all octaves
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # the checksum formula's numpy restatement (test infrastructure)
+
+    # incremental: cases already in checksums.json are kept (the 16384^2 dump alone is 7 GB); pass
+    # --force to regenerate every case
+    path = os.path.join(HERE, "checksums.json")
+    have = {}
+    if os.path.exists(path) and "--force" not in sys.argv:
+        with open(path) as f:
+            have = {(r["n"], r["S"], r["input"]): r for r in json.load(f)}
+    checks = []
+    for n, S, inp in CHECKSUM_CASES:
+        if (n, S, inp) in have:
+            checks.append(have[(n, S, inp)])
+            continue
+        pyr = dump(REF_SERIAL, "dump", n, S, inp)
+        sl, _ = level_slices(n, S)
+        acc, rec = 0, {"n": n, "S": S, "input": inp}
+        for o in range(octaves_of(n)):
+            m = n >> o
+            for s in range(S + 3):
+                off, _ = sl[(o, s)]
+                acc = (acc + oracle.level_checksum(pyr[off:off + m * m].reshape(m, m), o, s)) & 0xFFFFFFFFFFFFFFFF
+            rec[f"octaves_{o + 1}"] = f"{acc:016x}"
+        checks.append(rec)
+        print("checksum", n, inp, flush=True)
+    with open(os.path.join(HERE, "checksums.json"), "w") as f:
+        json.dump(checks, f, indent=1)
+
+
+def run_mpi(variant, n, S, inp):
+    """Collector-rank hashes of one multi-process reference run (S+4 ranks, rank S+3 prints)."""
+    binary = REF_MPI if variant.startswith("GaussDePyramid-MPI.h") else REF_MPITEST
+    args = [MPIEXEC, "-n", str(S + 4), binary, "hash", str(n), str(S), inp]
+    if binary == REF_MPITEST:
+        args.append("mpi_omp" if variant.endswith("_omp") else "mpi")
+    out = run(*args)
+    recs = [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+    assert len(recs) == 1, out
+    return recs[0]
+
+
+def gen_mpi():
+    for b in (REF_MPI, REF_MPITEST, REF_SERIAL):
+        if not os.path.exists(b):
+            sys.exit(f"missing {b}: run `make -C oracle ref ref-mpi` first")
+    out = []
+    for variant, n, S, inp in MPI_CASES:
+        rec = run_mpi(variant, n, S, inp)
+        ser = json.loads(run(REF_SERIAL, "hash", str(n), str(S), inp))
+        rec.update({"variant": variant, "input": inp, "ranks": S + 4, "collector_rank": S + 3,
+                    "equals_serial": rec["octaves"] == ser["octaves"]})
+        out.append(rec)
+        print("mpi", variant, n, S, inp, "equals serial:", rec["equals_serial"], flush=True)
+    with open(os.path.join(HERE, "mpi_hashes.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
+    parts = {"hashes", "dumps", "taps", "checksums", "mpi"}
+    if "--only" in sys.argv:
+        parts = set(sys.argv[sys.argv.index("--only") + 1].split(","))
+    if "mpi" in parts:
+        gen_mpi()
+    if not parts - {"mpi"}:
+        return
     for b in (REF_SERIAL, REF_AVX512):
         if not os.path.exists(b):
             sys.exit(f"missing {b}: run `make -C oracle ref` first")
+    if parts & {"hashes", "dumps", "taps"} != {"hashes", "dumps", "taps"} and parts & {"hashes", "dumps", "taps"}:
+        sys.exit("hashes, dumps and taps are generated together")
+    if "hashes" not in parts:
+        return gen_checksums() if "checksums" in parts else None
     hashes = []
     for n, S, inp in HASH_CASES:
         rec = json.loads(run(REF_SERIAL, "hash", str(n), str(S), inp))
@@ -148,26 +241,7 @@ def main():
     with open(os.path.join(HERE, "hashes.json"), "w") as f:
         json.dump(hashes, f, indent=1)
 
-    # gdp_checksum values (definition in include/gdp.h) of the reference's output for the bench's
-    # own input images, over the first 5 octaves (bench configs) and over all octaves
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle  # the checksum formula's numpy restatement (test infrastructure)
-
-    checks = []
-    for n, S, inp in CHECKSUM_CASES:
-        pyr = dump(REF_SERIAL, "dump", n, S, inp)
-        sl, _ = level_slices(n, S)
-        acc, rec = 0, {"n": n, "S": S, "input": inp}
-        for o in range(octaves_of(n)):
-            m = n >> o
-            for s in range(S + 3):
-                off, _ = sl[(o, s)]
-                acc = (acc + oracle.level_checksum(pyr[off:off + m * m].reshape(m, m), o, s)) & 0xFFFFFFFFFFFFFFFF
-            rec[f"octaves_{o + 1}"] = f"{acc:016x}"
-        checks.append(rec)
-        print("checksum", n, inp, flush=True)
-    with open(os.path.join(HERE, "checksums.json"), "w") as f:
-        json.dump(checks, f, indent=1)
+    gen_checksums()
     gxx = run("g++", "--version").splitlines()[0]
     meta = {
         "generator": "tests/golden/gen_golden.py via oracle/_ref/ref_serial + ref_avx512 "

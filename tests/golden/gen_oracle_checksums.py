@@ -20,7 +20,9 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 import oracle  # noqa: E402
 
 SEED = 0x5EED
-CASES = [(1080, 1920, 2, 5, 0), (1080, 1920, 2, 5, 1)]  # (H, W, S, O, image index) — bench config 3
+# (H, W, S, O, image index) — bench config 3: images 0 and 1, and the first and last image of every
+# rank at 64 images per GPU on up to 8 GPUs (bench.py verifies every rank's shard)
+CASES = [(1080, 1920, 2, 5, i) for i in sorted({0, 1} | {x for r in range(8) for x in (64 * r, 64 * r + 63)})]
 
 
 def main():

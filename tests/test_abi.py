@@ -101,7 +101,7 @@ def test_comm_library_exports_its_header(pkg):
     pkg.lib()  # torch first, then libgdp (the comm library links both)
     L = _comm_lib()
     names = pkg.header_functions(os.path.join(REPO, "include", "gdp_comm.h"))
-    assert len(names) == 8
+    assert len(names) == 9
     for n in names:
         assert hasattr(L, n), n
 
@@ -131,3 +131,112 @@ def test_conv_taps_of_the_extension_mode(pkg):
             assert R == min(6, max(1, math.ceil(3 * sig)))
             assert len(k) == 2 * R + 1 and abs(float(k.astype(np.float64).sum()) - 1) < 1e-6
             assert np.allclose(k, k[::-1]) and int(np.argmax(k)) == R
+
+
+class _Transfer(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int) for f in ("kind", "peer", "octave", "scale", "first_row", "rows", "cols")]
+
+
+SEND, RECV, COPY = 0, 1, 2
+
+
+def _plan(L, H, W, S, O, world, rank, root):
+    count = ctypes.c_int()
+    assert L.gdp_comm_plan(H, W, S, O, world, rank, root, None, 0, ctypes.byref(count)) in (0, 1)
+    buf = (_Transfer * max(1, count.value))()
+    assert L.gdp_comm_plan(H, W, S, O, world, rank, root, buf, count.value, ctypes.byref(count)) == 0
+    return [tuple(getattr(buf[i], f) for f, _ in _Transfer._fields_) for i in range(count.value)]
+
+
+def test_comm_plan_pairs_every_send_with_a_receive_and_tiles_the_pyramid(pkg):
+    """The RCCL collector's transfer schedule (gdp_comm_plan, what gdp_comm_gather_bands executes;
+    the counterpart of GaussDePyramid-MPI.h:285,298's per-row MPI_Send/MPI_Recv), checked without
+    GPUs: for world sizes 1..9 (empty bands included), odd H, octaves below and above 5 and any
+    root, rank r's sends equal the root's receives from r in order (RCCL matches one peer pair's
+    sends and receives in order), every receive / local copy lands at the band's rows, and the
+    root's receives + copies tile every level of the whole pyramid exactly once — the same rows
+    the Python collector assembles (distributed.band_level_rows / plan_band)."""
+    import importlib
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    L = _comm_lib()
+    for H, W, S, O in [(16384, 256, 2, 5), (97, 40, 2, 5), (100, 100, 2, 7), (33, 64, 1, 5), (4096, 128, 2, 13),
+                       (1080, 1920, 2, 5), (512, 512, 0, 3), (64, 96, 3, 6)]:
+        for world in range(1, 10):
+            for root in sorted({0, world - 1, world // 2}):
+                plans = [_plan(L, H, W, S, O, world, r, root) for r in range(world)]
+                root_plan = plans[root]
+                for r in range(world):
+                    r0, r1 = d.plan_band(H, world, r, O)
+                    levels = d.band_level_rows(H, O, r0, r1)
+                    want = [(o, s, first, rows, W >> o) for o, (first, rows) in enumerate(levels) if rows
+                            for s in range(S + 3)] if r1 > r0 else []
+                    if r == root:
+                        got = [t[2:] for t in root_plan if t[0] == COPY]
+                        assert all(t[1] == root for t in root_plan if t[0] == COPY)
+                    else:
+                        assert all(t[0] == SEND and t[1] == root for t in plans[r])
+                        got = [t[2:] for t in plans[r]]
+                        recv = [t[2:] for t in root_plan if t[0] == RECV and t[1] == r]
+                        assert recv == got, (H, world, root, r)
+                    assert got == want, (H, W, S, O, world, root, r)
+                cover = {}
+                for kind, _, o, s, first, rows, cols in root_plan:
+                    assert kind in (RECV, COPY) and cols == W >> o
+                    cover.setdefault((o, s), []).append((first, rows))
+                for o in range(O):
+                    for s in range(S + 3):
+                        spans = sorted(cover.get((o, s), []))
+                        pos = 0
+                        for first, rows in spans:
+                            assert first == pos, (H, world, root, o, s, spans)
+                            pos += rows
+                        assert pos == H >> o, (H, world, root, o, s, spans)
+
+
+def test_comm_plan_reports_capacity_and_bad_arguments(pkg):
+    L = _comm_lib()
+    count = ctypes.c_int(-1)
+    buf = (_Transfer * 2)()
+    assert L.gdp_comm_plan(4096, 4096, 2, 5, 2, 1, 0, buf, 2, ctypes.byref(count)) == 1  # 25 sends > 2
+    assert count.value == 25
+    assert L.gdp_comm_plan(4096, 4096, 2, 5, 2, 2, 0, buf, 2, ctypes.byref(count)) == 1  # rank out of range
+    assert L.gdp_comm_plan(4096, 4096, 2, 5, 2, 0, 2, buf, 2, ctypes.byref(count)) == 1  # root out of range
+
+
+_NOMEM_CHILD = r"""
+import ctypes, os, resource, sys
+L = ctypes.CDLL(sys.argv[1])
+L.gdp_last_error.restype = ctypes.c_char_p
+vm = [l for l in open("/proc/self/status") if l.startswith("VmSize:")][0]
+cur = int(vm.split()[1]) * 1024
+resource.setrlimit(resource.RLIMIT_AS, (cur + (1 << 30), resource.RLIM_INFINITY))
+ctx = ctypes.c_void_p()
+# 1 x 2^24 image, S = 60: a 63 x 2^24-float (4.2 GB) host tap table cannot be allocated under the limit
+rc = L.gdp_create(ctypes.byref(ctx), 1, 1 << 24, 60, 1, 1, 0)
+print(rc, ctx.value, L.gdp_last_error(None).decode())
+"""
+
+
+def test_allocation_failure_is_a_status_not_a_terminate(tmp_path):
+    """SURVEY.md §8(b): no C++ exception crosses the ABI.  A std::bad_alloc inside gdp_create
+    (host tap table past RLIMIT_AS) returns GDP_ERR_NOMEM with a message; the process lives on.
+    The tap table is planned on the host before the device probe, so this runs without a GPU."""
+    env = dict(os.environ, GDP_NO_TORCH="1")
+    r = subprocess.run(["python3", "-c", _NOMEM_CHILD, os.path.join(PKG, "lib", "libgdp.so")], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    rc, ptr, msg = r.stdout.strip().split(" ", 2)
+    assert rc == "4" and ptr == "None", r.stdout
+    assert "bad_alloc" in msg
+
+
+def test_window_centre_modes_are_exported(pkg):
+    from sift_parallel_optimization_amd._lib import GDP_CENTRE_INTLEN, GDP_CENTRE_SERIAL
+
+    L = pkg.lib()
+    assert (GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN) == (0, 1)
+    assert L.gdp_set_window_centre(None, 1) == 1
+    assert L.gdp_get_window_centre(None) == -1
+    assert L.gdp_copy_band(None, 0, None, 0, None) == 1
+    assert L.gdp_status_string(6) == b"internal error"

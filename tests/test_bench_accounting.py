@@ -42,3 +42,65 @@ def test_rotation_exceeds_the_infinity_cache():
     set_bytes = bench.algorithmic_bytes(4096, 4096, 2, 5, 1)
     rotate = max(1, -(-bench.ROTATE_BYTES // set_bytes))
     assert rotate == 5 and rotate * set_bytes >= 8 * (256 << 20)
+
+
+_RANK_PROBE = r"""
+import json, os, sys, time
+keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+with open(os.path.join(sys.argv[1], "rank%s.json" % os.environ["RANK"]), "w") as f:
+    json.dump({"env": {k: os.environ.get(k) for k in keys}, "argv": sys.argv[1:]}, f)
+if len(sys.argv) > 2 and sys.argv[2] == "fail-rank1":
+    if os.environ["RANK"] == "1":
+        sys.exit(3)
+    time.sleep(600)  # a rank left waiting in a collective: the launcher must stop it
+"""
+
+
+def test_bench_launches_its_own_ranks(tmp_path):
+    """`bench.py --gpus N` with no launcher starts N ranks itself: each child
+    gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT and the parent's
+    arguments; a failing rank's status is returned and the other ranks are stopped."""
+    import json
+    import time
+
+    import bench
+
+    probe = tmp_path / "probe.py"
+    probe.write_text(_RANK_PROBE)
+    assert bench.launch_ranks(3, [str(tmp_path), "ok"], script=str(probe)) == 0
+    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(3)]
+    ports = {r["env"]["MASTER_PORT"] for r in recs}
+    assert len(ports) == 1 and ports.pop().isdigit()
+    for r, rec in enumerate(recs):
+        assert rec["env"]["RANK"] == rec["env"]["LOCAL_RANK"] == str(r)
+        assert rec["env"]["WORLD_SIZE"] == rec["env"]["LOCAL_WORLD_SIZE"] == "3"
+        assert rec["env"]["MASTER_ADDR"] == "127.0.0.1"
+        assert rec["argv"] == [str(tmp_path), "ok"]
+    t0 = time.time()
+    assert bench.launch_ranks(2, [str(tmp_path), "fail-rank1"], script=str(probe)) == 3
+    assert time.time() - t0 < 60  # rank 0 (sleeping) was stopped, not waited for
+
+
+def _run_bench(env_extra, *args):
+    import subprocess
+
+    env = dict(os.environ, **env_extra)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], env=env, capture_output=True,
+                          text=True, timeout=300)
+
+
+def test_bench_rejects_a_world_size_that_differs_from_gpus():
+    r = _run_bench({"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, "--gpus", "2", "--no-cpu")
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_refuses_more_nccl_ranks_than_gpus():
+    """Under nccl (RCCL) every rank needs its own GPU: asking for more exits non-zero with a
+    message instead of silently running fewer ranks (here: no GPU at all)."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("enough GPUs visible")
+    r = _run_bench({"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "GDP_BENCH_BACKEND": "nccl"},
+                   "--gpus", "2", "--no-cpu")
+    assert r.returncode != 0 and "need 2 GPUs" in r.stderr

@@ -607,43 +607,166 @@ def test_cpp_dropin_driver_matches_reference(oracle, golden, tmp_path):
     assert len(timing) == 2 and all(float(t.split()[0]) > 0 for t in timing), timing
 
 
-def test_cpp_mpitest_dropin_matches_oracle(oracle, tmp_path):
-    """mpitest.cpp's free-function API (GaussPyInit(int**), GenerateDoG_mpi_omp, delete_mpi)."""
+def _mpi_records(variant):
+    import json
+
+    with open(os.path.join(REPO, "tests", "golden", "mpi_hashes.json")) as f:
+        return [r for r in json.load(f) if r["variant"] == variant]
+
+
+def _assert_hashes(oracle, pyr, rec, what):
+    n, S = rec["n"], rec["S"]
+    lv = oracle.levels(pyr, n, n, S, oracle.octaves(n))
+    for o, row in enumerate(rec["octaves"]):
+        for s, h in enumerate(row):
+            assert oracle.fnv(lv[(o, s)]) == int(h, 16), (what, n, S, rec["input"], o, s)
+
+
+def test_cpp_mpitest_dropin_matches_the_reference_mpitest(oracle, tmp_path):
+    """mpitest.cpp's free-function API (GaussPyInit(int**), GenerateDoG_mpi / _mpi_omp, delete_mpi)
+    on the GPU == the collector's pyramid of mpitest.cpp ITSELF run under mpiexec with S+4 ranks
+    (tests/golden/mpi_hashes.json), for every n — including n = 100 / 1000 / 96, where its
+    integer-length window centre differs from the serial header."""
     exe = os.path.join(REPO, "examples", "mpitest_hip")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
     out = tmp_path / "m.f32"
-    for n, spec in [(256, "lcg:12345"), (256, "ones"), (100, "lcg:3")]:
-        r = subprocess.run([exe, str(n), spec, str(out)], check=True, timeout=120, capture_output=True, text=True)
-        assert float(r.stdout.split()[0]) >= 0  # elapsed seconds, printed like the collector rank
-        _assert_same(np.fromfile(out, dtype=np.float32), oracle.build_pyramid(oracle.image_from_spec(n, spec), 2),
-                     ("mpitest", n, spec))
+    for fn in ("mpi", "mpi_omp"):
+        recs = _mpi_records("mpitest.cpp:GenerateDoG_" + fn)
+        assert len(recs) >= 6
+        for rec in recs:
+            n, S, spec = rec["n"], rec["S"], rec["input"]
+            r = subprocess.run([exe, str(n), spec, str(out), fn, str(S)], check=True, timeout=120, capture_output=True,
+                               text=True)
+            assert float(r.stdout.split()[0]) >= 0  # elapsed seconds, printed like the collector rank
+            got = np.fromfile(out, dtype=np.float32)
+            _assert_hashes(oracle, got, rec, ("mpitest", fn))
+            _assert_same(got, oracle.build_pyramid(oracle.image_from_spec(n, spec), S, centre="intlen"),
+                         ("mpitest vs oracle", fn, n))
+            if not rec["equals_serial"]:  # the documented difference from GuassDePyramid.h, explicitly
+                assert not np.array_equal(_bits(got), _bits(oracle.build_pyramid(oracle.image_from_spec(n, spec), S)))
 
 
 def test_cpp_mpi_variant_dropin_collector(oracle, golden, tmp_path):
     """GaussPyramid_hip_mpi (GaussDePyramid-MPI.h's class, MPI as launcher + RCCL collector):
-    the collector's GaussPy after GenerateDoG_mpi == the reference, as an MPI singleton and under
-    mpiexec -n 1 (one GPU on the box; ranks > 1 need one GPU each — RCCL rejects two ranks on
-    one device)."""
+    the collector's GaussPy after GenerateDoG_mpi == GaussPyramid_mpi::GenerateDoG_mpi's collector
+    run under mpiexec with S+4 ranks (tests/golden/mpi_hashes.json) for every n, as an MPI
+    singleton and under mpiexec -n 1 (one GPU on the box; ranks > 1 need one GPU each — RCCL
+    rejects two ranks on one device).  Repeated calls continue from the current contents:
+    re-entry on the bands (2 and 3 calls) and after a single-process GenerateDoG ("mixed")."""
     exe = os.path.join(REPO, "examples", "mpi_hip")
     mpiexec = "/opt/conda/bin/mpiexec"
     if not os.path.exists(exe):
         pytest.skip("examples/mpi_hip not built (no MPI headers at build time)")
-    rec = [r for r in golden["hashes"] if r["n"] == 512 and r["input"] == "lcg:12345"][0]
     out = tmp_path / "c.f32"
-    cmds = [[exe, "512", "lcg:12345", str(out)]]
-    if os.path.exists(mpiexec):
-        cmds.append([mpiexec, "-n", "1", exe, "512", "lcg:12345", str(out)])
-    for cmd in cmds:
-        if out.exists():
-            out.unlink()
-        subprocess.run(cmd, check=True, timeout=180, capture_output=True)
-        lv = oracle.levels(np.fromfile(out, dtype=np.float32), 512, 512, 2, 10)
-        for o, row in enumerate(rec["octaves"]):
-            for s, h in enumerate(row):
-                assert oracle.fnv(lv[(o, s)]) == int(h, 16), (cmd[0], o, s)
-    subprocess.run([exe, "100", "lcg:3", str(out)], check=True, timeout=180, capture_output=True)
-    _assert_same(np.fromfile(out, dtype=np.float32), oracle.build_pyramid(oracle.lcg_image(100, 100, 3), 2), "mpi 100")
+    recs = [r for r in _mpi_records("GaussDePyramid-MPI.h:GenerateDoG_mpi") if r["S"] == 2]
+    assert len(recs) >= 4
+    for rec in recs:
+        n, spec = rec["n"], rec["input"]
+        cmds = [[exe, str(n), spec, str(out)]]
+        if os.path.exists(mpiexec) and n == 512:
+            cmds.append([mpiexec, "-n", "1", exe, str(n), spec, str(out)])
+        for cmd in cmds:
+            if out.exists():
+                out.unlink()
+            subprocess.run(cmd, check=True, timeout=180, capture_output=True)
+            _assert_hashes(oracle, np.fromfile(out, dtype=np.float32), rec, cmd[0])
+    n, spec, S = 100, "lcg:3", 2
+    img = oracle.image_from_spec(n, spec)
+    O = oracle.octaves(n)
+    for calls, mode in [(2, "mpi"), (3, "mpi"), (2, "mixed"), (3, "mixed")]:
+        subprocess.run([exe, str(n), spec, str(out), str(calls), mode], check=True, timeout=180, capture_output=True)
+        want = oracle.init_pyramid(img, S)
+        for c in range(calls):
+            if c > 0 and mode == "mixed":
+                oracle.generate_dog(want, n, n, S, O)  # single-process GenerateDoG: serial centre
+            oracle.generate_dog(want, n, n, S, O, centre="intlen")
+        _assert_same(np.fromfile(out, dtype=np.float32), want, ("mpi re-entry", calls, mode))
+
+
+def test_reference_drivers_run_on_the_dropin(tmp_path):
+    """The reference's own main.cpp (two-line switch) and mpitest.cpp
+    (definitions deleted per §3), compiled in the container by `make -C oracle dropin` from the
+    unmodified reference files, run to completion on the GPU and print their timings."""
+    ref = os.path.join(REPO, "oracle", "_ref")
+    main, mpi, mpitest = (os.path.join(ref, x) for x in ("dropin_main", "dropin_main_mpi", "dropin_mpitest"))
+    if not os.path.exists(main):
+        pytest.skip("oracle/_ref/dropin_* not built (needs the reference sources at build time)")
+    r = subprocess.run([main], check=True, timeout=180, capture_output=True, text=True)
+    assert float(r.stdout.split()[-1]) > 0  # main.cpp:74 mean ms per GenerateDoG_mpi call
+    r = subprocess.run([mpitest], check=True, timeout=180, capture_output=True, text=True)
+    assert float(r.stdout.split()[-1]) >= 0  # elapsed seconds (mpitest.cpp:95-96)
+    if os.path.exists(mpi):
+        for cmd in ([mpi], ["/opt/conda/bin/mpiexec", "-n", "1", mpi]):
+            if cmd[0].startswith("/opt") and not os.path.exists(cmd[0]):
+                continue
+            r = subprocess.run(cmd, check=True, timeout=180, capture_output=True, text=True)
+            assert float(r.stdout.split()[-1]) > 0
+
+
+@pytest.mark.parametrize("H,W,O,batch,band", [(100, 100, 0, 1, None), (96, 160, 0, 2, None), (1000, 1000, 0, 1, None),
+                                               (300, 200, 5, 1, (16, 272)), (97, 97, 0, 1, None)])
+def test_intlen_window_centre(pkg, oracle, H, W, O, batch, band):
+    """GDP_CENTRE_INTLEN (the MPI variants' centre) == the oracle's restatement, which
+    tests/test_oracle.py pins to the reference's own MPI runs; switching back restores the serial
+    taps bit for bit."""
+    imgs = [oracle.lcg_image(H, W, 40 + b) for b in range(batch)]
+    r0, r1 = band or (0, H)
+    with pkg.PyramidContext(H, W, S=2, octaves=O, batch=batch, row_begin=r0, row_end=r1, centre="intlen") as ctx:
+        for b, im in enumerate(imgs):
+            ctx.set_input(im[r0:r1], b)
+        for centre in ("intlen", "serial", "intlen"):
+            ctx.set_window_centre(centre)
+            ctx.build()
+            ctx.sync()
+            for b, im in enumerate(imgs):
+                want = oracle.levels(oracle.build_pyramid(im, 2, ctx.O, centre=centre), H, W, 2, ctx.O)
+                for (o, s), lev in want.items():
+                    rows, cols, first = ctx.level_dims(o)
+                    _assert_same(ctx.level(b, o, s), lev[first:first + rows], (centre, b, o, s))
+            for o in range(ctx.O):
+                _assert_same(ctx.taps(0, o, 1), oracle.taps(W, o, 1, centre=centre), ("taps", centre, o))
+
+
+def test_copy_band_from_whole_image(pkg, oracle):
+    """gdp_copy_band: a band context takes its rows of a whole-image context's current pyramid,
+    then re-enters (GenerateDoG) exactly like the whole image does on those rows."""
+    H, W, S = 512, 384, 2
+    img = oracle.lcg_image(H, W, 9)
+    with pkg.PyramidContext(H, W, S=S, octaves=5) as full, \
+            pkg.PyramidContext(H, W, S=S, octaves=5, row_begin=128, row_end=384) as band:
+        full.set_input(img)
+        full.build()
+        band.copy_band_from(full)
+        full.generate_dog()
+        band.generate_dog()
+        full.sync()
+        band.sync()
+        for o in range(5):
+            rows, cols, first = band.level_dims(o)
+            for s in range(S + 3):
+                _assert_same(band.level(0, o, s), full.level(0, o, s)[first:first + rows], ("band", o, s))
+
+
+def test_config4_shard_64_images_4096(pkg, golden):
+    """Config 4's per-GPU workload: 64 x 4096^2 (28.6 GB of pyramid) in ONE context, the images
+    rank 0 (global 0..63) and rank 7 (448..511) of the 8-GPU split own, generated on the device;
+    the first and last image of each shard against the checksum of the reference's own output
+    (global indices past 2^32 pixels exercise the counter hash's folded index)."""
+    want = {int(r["input"].split(":")[2]): int(r["octaves_5"], 16) for r in golden["checksums"]
+            if r["n"] == 4096 and r["input"].startswith("synth:0x5EED:")}
+    with pkg.PyramidContext(4096, 4096, S=2, octaves=5, batch=64) as ctx:
+        assert ctx.pyramid_bytes() > 28 << 30
+        for first in (0, 448):
+            ctx.fill_synthetic(0x5EED, first)
+            ctx.build()
+            ctx.sync()
+            for b in (0, 63):
+                assert ctx.checksum(b) == want[first + b], (first, b)
+            if first == 0:  # and every other image of rank 0's shard that has a fixture
+                for b in range(1, 63):
+                    if b in want:
+                        assert ctx.checksum(b) == want[b], b
 
 
 # ------------------------------------------------------------------ extension: true Gaussian convolution
