@@ -363,6 +363,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None,
                     help="force a build-kernel variant (and skip autotuning), e.g. for profiling runs")
+    ap.add_argument("--tile-order", type=int, default=None,
+                    help="with --variant: force the build tile order too (0 linear, 1 XCD-chunked)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
@@ -458,7 +460,7 @@ def main():
     autotuned = None
     if args.variant is not None:
         for c in ctxs:
-            c.set_tuning(variant=args.variant)
+            c.set_tuning(variant=args.variant, tile_order=args.tile_order)
     elif args.op == "build" and not args.no_autotune:
         # candidates interleaved round-robin (drift hits all alike), over the rotated sets
         autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10)

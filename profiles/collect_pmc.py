@@ -9,8 +9,10 @@ Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE
 are KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read,
 so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
 
-Writes profiles/pmc_<config>_<round>.json (read by bench.py for roofline.traffic) and copies the
-kernel-stats CSV to profiles/rocprof_<config>_<round>_kernel_stats.csv.
+Writes profiles/pmc_<tag>_<round>.json (read by bench.py for roofline.traffic when the run's build
+variant and tile order equal the recorded ones) and copies the kernel-stats CSV to
+profiles/rocprof_<tag>_<round>_kernel_stats.csv.  The profiled bench runs are forced to one
+variant / tile order (bench.py --variant V --tile-order T), recorded here.
 """
 import argparse
 import csv
@@ -44,6 +46,9 @@ def main():
     ap.add_argument("--bench-json", help="bench.py output line of the traced run (optional)")
     ap.add_argument("--kernel", default="k_build", help="substring of the kernel to summarise")
     ap.add_argument("--op", default="build", help="bench.py --op of the profiled run")
+    ap.add_argument("--variant", type=int, required=True, help="build variant the profiled runs were forced to")
+    ap.add_argument("--tile-order", type=int, required=True, help="build tile order of the profiled runs")
+    ap.add_argument("--tag", default=None, help="file tag (default: config, or config_op)")
     args = ap.parse_args()
 
     import bench
@@ -65,6 +70,7 @@ def main():
     write_b = statistics.median(write) * 1024
     rec = {
         "config": args.config, "round": args.round, "kernel": name,
+        "variant": args.variant, "tile_order": args.tile_order, "input_format": "i32",
         "trace_calls": int(stats["Calls"]) if stats else None,
         "trace_avg_ns": float(stats["AverageNs"]) if stats else None,
         "trace_min_ns": float(stats["MinNs"]) if stats else None,
@@ -96,7 +102,7 @@ def main():
             rec["trace_timed_steps"] = len(timed)
             rec["trace_timed_avg_ns"] = statistics.mean(timed)
             rec["bench_kernel_ms"] = line["roofline"]["kernel_ms"]
-    tag = args.config if args.op == "build" else f"{args.config}_{args.op}"
+    tag = args.tag or (args.config if args.op == "build" else f"{args.config}_{args.op}")
     rec["op"] = args.op
     out = os.path.join(HERE, f"pmc_{tag}_{args.round}.json")
     with open(out, "w") as f:
