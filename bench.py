@@ -374,9 +374,13 @@ def main():
                     help="build: fused GaussPyInit+GenerateDoG (headline); regen: in-place GenerateDoG "
                          "re-entry; gauss: in-place row+column window pass of every octave; conv: the "
                          "true-Gaussian-convolution extension (not the reference's algorithm)")
-    ap.add_argument("--conv-kernel", type=int, default=None, help="--op conv: 0 register sweep, 1 LDS tiles")
-    ap.add_argument("--conv-rows", type=int, default=None, help="--op conv sweep: rows per wave strip (16/32)")
-    ap.add_argument("--conv-order", type=int, default=None, help="--op conv sweep: bit 0 XCD-chunked, bit 1 alternate directions")
+    ap.add_argument("--conv-kernel", type=int, default=None,
+                    help="--op conv: 0 register sweep, 1 LDS tiles, 2 block tiles (default)")
+    ap.add_argument("--conv-rows", type=int, default=None,
+                    help="--op conv: block tiles' rows per block (32 default) / the sweep's rows per strip (16/32)")
+    ap.add_argument("--conv-order", type=int, default=None,
+                    help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
+                         "after their input rows; default 4)")
     ap.add_argument("--scatter", action="store_true",
                     help="N > 1, image configs: also measure the image-batch split (rank 0's batch scattered over "
                          "RCCL, SURVEY.md §8e), outside the timed region, and check the ranks build the same bits from it")
@@ -557,7 +561,10 @@ def main():
                        if args.op == "build" else
                        {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
                         "gauss": "k_window (in-place row+column window, all octaves)",
-                        "conv": ("k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
+                        "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
+                                 "240-column block tiles, one output row per wave, DPP lane shifts)" % ctx.tuning()["conv_rows"]
+                                 if ctx.tuning()["conv_kernel"] == 2 and S <= 3 else
+                                 "k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
                                  "DPP lane shifts, %d-row strips)" % ctx.tuning()["conv_rows"]
                                  if ctx.tuning()["conv_kernel"] == 0 and S <= 3 else
                                  "k_conv (extension: separable Gaussian convolution, LDS halo tiles)")}[args.op]),

@@ -223,19 +223,22 @@ enum {
     GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk
                                    (1 default, 2 or 4); 0 = one level per wave (k_levels_x) */
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
-    GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (default, S <= 3), 1 LDS tiles */
-    GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian sweep: output rows per wave strip (16 default, 32) */
-    GDP_TUNE_CONV_ORDER = 11,   /* gdp_build_gaussian sweep: bit 0 XCD-chunked block order, bit 1 odd waves
-                                   sweep bottom-up (shared halo rows loaded together), bit 2 octave
+    GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (S <= 3), 1 LDS tiles,
+                                   2 block tiles (default; one output row per wave, S <= 3) */
+    GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian: block tiles' rows per block (32 default;
+                                   16 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8); the sweep's
+                                   rows per wave strip (16 / 32) */
+    GDP_TUNE_CONV_ORDER = 11,   /* gdp_build_gaussian block order: bit 0 XCD-chunked, bit 1 odd
+                                   sweep waves go bottom-up (sweep only), bit 2 (default 4) octave
                                    o's block rows issued right after the octave-0 rows covering
-                                   their input rows; default 5 for batches, 4 for one
-                                   image >= 64 Mpix, 0 for smaller single images */
+                                   their input rows */
     GDP_TUNE_BUILD_LDS = 12,    /* gdp_build: dynamic LDS bytes requested per block (0 default);
                                    used only to cap resident blocks per CU (occupancy) */
     GDP_TUNE_STAGE_KB = 13,     /* row-pointer downloads: KiB per half of the double-buffered
                                    pinned staging buffer (32768 default) */
-    GDP_TUNE_STAGE_THREADS = 14 /* row-pointer downloads: host threads scattering a staged batch
+    GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
                                    into the caller's rows (4 default) */
+    GDP_TUNE_CONV_WAVES = 15    /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

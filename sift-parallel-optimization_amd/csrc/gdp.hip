@@ -91,16 +91,18 @@ struct gdp_ctx {
     const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
     float* d_taps = nullptr;
-    int conv_kernel = 0;          // GDP_TUNE_CONV_KERNEL: 0 register sweep (default), 1 LDS tiles
-    int conv_rows = 16;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep
-    int conv_order = 5;           // GDP_TUNE_CONV_ORDER (default set per geometry in gdp_create): bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
-                                  // bit 2 input-row-interleaved octaves (conv_sweep_perm)
+    int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
+    int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
+    int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
+    int conv_order = 4;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
+                                  // bit 2 input-row-interleaved octaves (conv_sweep_perm; default 4)
     int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
     int centre_mode = GDP_CENTRE_SERIAL; // gdp_set_window_centre
     float* d_ctaps = nullptr;     // convolution-mode taps [L][13] (extension)
     int* d_cradius = nullptr;     // convolution-mode radius per scale
     unsigned* d_conv_perm = nullptr; // conv sweep block order for GDP_TUNE_CONV_ORDER bit 2 (per image)
     bool conv_perm_dirty = true;
+    int conv_perm_kernel = -1;       // the conv kernel d_conv_perm was built for (its block prefix)
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
     float* h_stage = nullptr;     // pinned staging for row-pointer downloads (two halves)
     size_t h_stage_floats = 0;
@@ -259,54 +261,60 @@ bool valid_level(const gdp_ctx* c, int b, int o, int s) {
 // ==========================================================================================
 // C ABI
 // ==========================================================================================
-// Block prefix of the convolution sweep (kSwWaves strips of conv_rows rows x kSwCols columns).
+// Block prefixes of the convolution sweep (kSwWaves strips of conv_rows rows x kSwCols columns)
+// and of the block tiles (conv_block_rows() rows x kSwCols columns).
+static int conv_block_rows(const gdp_ctx* c) { return c->conv_rows != 16 ? c->conv_rows : 16; }
+static int conv_sweep_rows(const gdp_ctx* c) { return c->conv_rows == 32 ? 32 : 16; }
 static void conv_sweep_geom(gdp_ctx* c) {
     Geom& g = c->geom;
     const int strip_cols = SwGeom<kSwV>::kCols;
     g.sw_blk[0] = 0;
     g.cvx_blk[0] = 0;
+    g.bk_blk[0] = 0;
     for (int o = 0; o < g.O; ++o) {
         const OctGeom& og = g.oct[o];
         const bool sweep = og.cols >= 4 && og.cols % 4 == 0; // full-vector stores on every row
         g.sw_strips_c[o] = (og.cols + strip_cols - 1) / strip_cols;
-        const long long rows_per_blk = (long long)kSwWaves * c->conv_rows;
+        const long long rows_per_blk = (long long)kSwWaves * conv_sweep_rows(c);
         g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
+        const long long bk_rows = conv_block_rows(c);
+        g.bk_blk[o + 1] = g.bk_blk[o] + (sweep ? (unsigned)((og.rows + bk_rows - 1) / bk_rows * g.sw_strips_c[o]) : 0u);
         g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
     }
     c->conv_perm_dirty = true;
 }
 
-// Input-row-interleaved block order of the convolution sweep (GDP_TUNE_CONV_ORDER bit 2): each
-// octave-o block row (kSwWaves * conv_rows output rows = 2^o times as many input rows) is issued
-// right after the octave-0 block row that covers the last of its input rows, so the decimated
-// rows it reads were just brought on chip by octave 0 instead of being fetched again.
-static int conv_sweep_perm(gdp_ctx* c) {
+// Input-row-interleaved block order of the convolution sweep / block tiles (GDP_TUNE_CONV_ORDER
+// bit 2): each octave-o block row (2^o times as many input rows as an octave-0 block row) is
+// issued right after the octave-0 block row that covers the last of its input rows, so the
+// decimated rows it reads were just brought on chip by octave 0 instead of being fetched again.
+// `blk` is the block prefix of the kernel that will run (sw_blk or bk_blk).
+static int conv_sweep_perm(gdp_ctx* c, const unsigned* blk) {
     const Geom& g = c->geom;
     std::vector<unsigned> perm;
-    perm.reserve(g.sw_blk[g.O]);
+    perm.reserve(blk[g.O]);
     auto emit_row = [&](int o, unsigned tr) {
         const unsigned sc = (unsigned)g.sw_strips_c[o];
-        for (unsigned tc = 0; tc < sc; ++tc) perm.push_back(g.sw_blk[o] + tr * sc + tc);
+        for (unsigned tc = 0; tc < sc; ++tc) perm.push_back(blk[o] + tr * sc + tc);
     };
-    const unsigned rows0 = g.oct[0].cols ? (g.sw_blk[1] - g.sw_blk[0]) / std::max(1u, (unsigned)g.sw_strips_c[0]) : 0;
+    const unsigned rows0 = g.oct[0].cols ? (blk[1] - blk[0]) / std::max(1u, (unsigned)g.sw_strips_c[0]) : 0;
     std::vector<unsigned> next(g.O, 0); // next block row of each octave
     for (unsigned k = 0; k < rows0; ++k) {
         emit_row(0, k);
         for (int o = 1; o < g.O; ++o) {
             const unsigned sc = (unsigned)std::max(1, g.sw_strips_c[o]);
-            const unsigned nrows = (g.sw_blk[o + 1] - g.sw_blk[o]) / sc;
+            const unsigned nrows = (blk[o + 1] - blk[o]) / sc;
             // octave-o block row tr covers octave-0 block rows [2^o tr, 2^o (tr + 1))
             while (next[o] < nrows && ((unsigned long long)(next[o] + 1) << o) <= (unsigned long long)k + 1)
                 emit_row(o, next[o]++);
         }
     }
-    for (int o = 0; o < g.O; ++o) { // leftovers (octave 0 swept nothing, or rounding at the bottom)
+    for (int o = 1; o < g.O; ++o) { // leftovers (octave 0 swept nothing, or rounding at the bottom)
         const unsigned sc = (unsigned)std::max(1, g.sw_strips_c[o]);
-        const unsigned nrows = (g.sw_blk[o + 1] - g.sw_blk[o]) / sc;
-        if (o == 0) continue;
+        const unsigned nrows = (blk[o + 1] - blk[o]) / sc;
         while (next[o] < nrows) emit_row(o, next[o]++);
     }
-    if (perm.size() != g.sw_blk[g.O]) return c->status(GDP_ERR_STATE, "conv sweep order: %zu of %u blocks", perm.size(), g.sw_blk[g.O]);
+    if (perm.size() != blk[g.O]) return c->status(GDP_ERR_STATE, "conv block order: %zu of %u blocks", perm.size(), blk[g.O]);
     if (c->d_conv_perm) GDP_HIP(c, hipFree(c->d_conv_perm));
     c->d_conv_perm = nullptr;
     if (!perm.empty()) {
@@ -326,9 +334,38 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     return hipGetLastError();
 }
 
+template <int L, int T, int W>
+hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
+    auto k = k_conv_blk<L, T, W>;
+    const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
+                       c->d_conv_perm);
+    return hipGetLastError();
+}
+
+// block tiles: (rows per block, waves per block) pairs that are instantiated
+template <int L>
+hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
+    const int T = conv_block_rows(c), W = c->conv_waves;
+    if (W == 8 || T == 8 || T == 24) { // 8- and 24-row tiles are whole rows per wave only with 8 waves
+        switch (T) {
+            case 8: return launch_conv_blk_t<L, 8, 8>(c, units, st);
+            case 16: return launch_conv_blk_t<L, 16, 8>(c, units, st);
+            case 24: return launch_conv_blk_t<L, 24, 8>(c, units, st);
+            default: return launch_conv_blk_t<L, 32, 8>(c, units, st);
+        }
+    }
+    switch (T) {
+        case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
+        case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
+        default: return launch_conv_blk_t<L, 16, 16>(c, units, st);
+    }
+}
+
 template <int L>
 hipError_t launch_conv_sweep_l(gdp_ctx* c, unsigned grid, hipStream_t st) {
-    return c->conv_rows == 32 ? launch_conv_sweep_t<L, 32>(c, grid, st) : launch_conv_sweep_t<L, 16>(c, grid, st);
+    if (c->conv_kernel == 2) return launch_conv_blk<L>(c, grid, st);
+    return conv_sweep_rows(c) == 32 ? launch_conv_sweep_t<L, 32>(c, grid, st) : launch_conv_sweep_t<L, 16>(c, grid, st);
 }
 
 // ---- no C++ exception crosses the C ABI --------------------------------------------------------
@@ -409,14 +446,13 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     try {
     c->device = device;
     c->variant = default_variant(W, (long long)(row_end - row_begin) * W, batch);
-    // Convolution-extension block order (tools/tune.py --op conv, cold buffers): batches 5 (XCD-
-    // chunked + octave rows after the octave-0 rows that hold their inputs: 64 x 4096^2 6.28 vs
-    // 7.00 ms linear), one large image 4 (the interleave without XCD chunking: 16384^2 1.59 vs
-    // 1.80 for 5), one image <= 64 Mpix 0 (linear: 4096^2 0.119 vs 0.128 for 5).
-    {
-        const long long px = (long long)(row_end - row_begin) * W;
-        c->conv_order = batch > 1 ? 5 : (px >= (1ll << 26) ? 4 : 0);
-    }
+    // Convolution extension default: block tiles of 32 rows (16 waves) in block order 4 (octave-o
+    // block rows right after the octave-0 rows that hold their input rows, no XCD chunking) —
+    // the fastest form on every config (tools/conv_ab.sh, cold buffers: 4096^2 0.111 ms vs 0.119
+    // for the sweep, 64 x 1080x1920 0.795 vs 0.809, 64 x 4096^2 6.34 vs 6.79, 16384^2 1.62 vs 1.72).
+    c->conv_kernel = 2;
+    c->conv_rows = 32;
+    c->conv_order = 4;
     Geom& g = c->geom;
     g.H = H;
     g.W = W;
@@ -435,6 +471,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
 
     // optional padding between levels (floats, multiple of 64) — layout experiment knob
     const char* pad_env = std::getenv("GDP_LEVEL_PAD");
+    if (const char* d = std::getenv("GDP_CONV_DIAG")) g.diag = std::atoi(d);
     const long long level_pad = pad_env ? round_up(std::max(0ll, std::atoll(pad_env)), kLevelAlign) : 0;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
     long long tap_off = 0, lev_off = 0, grp = 0;
@@ -753,13 +790,15 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     const hipStream_t st = c->pick(stream);
     // the register sweep is compiled for S = 0..3 (L = 3..6) and takes the octaves whose width is a
     // multiple of 4; the LDS tiles take the rest (and everything for other S or conv_kernel = 1)
-    const bool sweep = c->conv_kernel == 0 && g.L >= 3 && g.L <= 6;
-    if (sweep && (c->conv_order & 4) && c->conv_perm_dirty) {
-        const int rc = conv_sweep_perm(c);
+    const bool sweep = c->conv_kernel != 1 && g.L >= 3 && g.L <= 6;
+    const unsigned* blk = c->conv_kernel == 2 ? g.bk_blk : g.sw_blk;
+    if (sweep && (c->conv_order & 4) && (c->conv_perm_dirty || c->conv_perm_kernel != c->conv_kernel)) {
+        const int rc = conv_sweep_perm(c, blk);
         if (rc != GDP_OK) return rc;
+        c->conv_perm_kernel = c->conv_kernel;
     }
     if (sweep) {
-        const long long grid = (long long)g.sw_blk[g.O] * g.batch;
+        const long long grid = (long long)blk[g.O] * g.batch;
         if (grid >= (1ll << 31) - 8) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
         if (grid > 0) {
             switch (g.L) {
@@ -1141,6 +1180,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_CONV_KERNEL: *value = c->conv_kernel; return GDP_OK;
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
+        case GDP_TUNE_CONV_WAVES: *value = c->conv_waves; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -1170,11 +1210,14 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
         case GDP_TUNE_CONV_KERNEL:
-            if (value != 0 && value != 1) return c->status(GDP_ERR_ARG, "conv kernel must be 0 (sweep) or 1 (tiles)");
+            if (value < 0 || value > 2)
+                return c->status(GDP_ERR_ARG, "conv kernel must be 0 (sweep), 1 (LDS tiles) or 2 (block tiles)");
             c->conv_kernel = value;
             return GDP_OK;
         case GDP_TUNE_CONV_ROWS: {
-            if (value != 16 && value != 32) return c->status(GDP_ERR_ARG, "conv rows must be 16 or 32");
+            if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48)
+                return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32 or 48 (sweep: 16 / 32; block tiles: "
+                                              "16 / 32 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8)");
             const int old = c->conv_rows;
             c->conv_rows = value;
             conv_sweep_geom(c);
@@ -1185,6 +1228,10 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             }
             return rc;
         }
+        case GDP_TUNE_CONV_WAVES:
+            if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
+            c->conv_waves = value;
+            return GDP_OK;
         case GDP_TUNE_CONV_ORDER:
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;
