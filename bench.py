@@ -352,6 +352,28 @@ def verify(ctx, cfg, key, world, rank, dist, mg, first_image):
                         "oracle closed form (non-square input: no reference output exists)")}
 
 
+def verify_conv_bands(ctx, cfg, world, rank, dist, mg, in_fmt):
+    """Convolution extension on row bands (no reference output exists for this mode): the sum of
+    every rank's band checksum must equal the checksum of the whole image built on ONE GPU (rank
+    0, after the timed region) — the halo exchange delivered exactly the rows the bands read."""
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    sums = mg.gather_checksums([ctx.checksum(0)], dist=dist)
+    if rank != 0:
+        return None
+    got = sum(v[0] for v in sums) & 0xFFFFFFFFFFFFFFFF
+    with pkg.PyramidContext(cfg["H"], cfg["W"], S=2, octaves=cfg["O"], batch=1, device=ctx.device,
+                            input_format=in_fmt) as whole:
+        whole.fill_synthetic(SEED, 0)
+        whole.build_gaussian()
+        whole.sync()
+        want = whole.checksum(0)
+    return {"status": "bands == whole image (bit-exact)" if got == want else "MISMATCH",
+            "checked": f"sum of {world} row-band checksums (halo rows exchanged every step) vs the whole image "
+                       f"built on one GPU", "checksum": f"{got:016x}", "whole_image_checksum": f"{want:016x}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -444,9 +466,29 @@ def main():
         units_all = world * B * H * W
         set_bytes = algorithmic_bytes(H, W, S, O, B, in_bytes)
     rotate = args.rotate or max(1, -(-ROTATE_BYTES // max(1, set_bytes)))
-    ctxs = []
+    # the convolution extension on row bands reads its neighbours' rows: each band's input lives in
+    # a torch tensor (the rows its neighbours need are sent from it) and its halo rows are received
+    # into bound tensors by distributed.exchange_halo — RCCL point-to-point over xGMI, part of every
+    # timed step (the reference's pointwise window needs no exchange)
+    halo_exchange = args.op == "conv" and cfg["band"] and world > 1
+    ctxs, halos = [], []
     for _ in range(rotate):  # identical sets (same images) at different addresses
         c = make()
+        if halo_exchange:
+            dev = torch.device("cuda", local)
+            edt = torch.uint8 if args.input == "u8" else torch.int32
+            inp = torch.empty((1, r1 - r0, W), dtype=edt, device=dev)
+            c.bind_device_input(inp.data_ptr(), W, (r1 - r0) * W, keepalive=inp)
+            above, below = c.conv_halo_rows()
+            top = torch.empty((1, max(above, 1), W), dtype=edt, device=dev)
+            bot = torch.empty((1, max(below, 1), W), dtype=edt, device=dev)
+            c.bind_input_halo(top.data_ptr() if above else None, bot.data_ptr() if below else None, pitch=W,
+                              keepalive=(top, bot))
+            # gloo rehearsals exchange through host memory: a host image of the band, refreshed
+            # only in the rows the neighbours need, and host halo buffers
+            host = ((torch.empty(inp.shape, dtype=edt), torch.empty(top[:, :above].shape, dtype=edt),
+                     torch.empty(bot[:, :below].shape, dtype=edt)) if backend != "nccl" else None)
+            halos.append((inp, top[:, :above], bot[:, :below], host))
         c.fill_synthetic(SEED, first_image)
         ctxs.append(c)
     ctx = ctxs[0]
@@ -470,6 +512,22 @@ def main():
         autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10)
     if args.op == "build":
         steps_fn = [c.build for c in ctxs]
+    elif args.op == "conv" and halo_exchange:
+        def conv_step(i, st):
+            inp, top, bot, host = halos[i]
+            if backend == "nccl":
+                mg.exchange_halo(inp, top, bot, H, world, rank, O, dist=dist)
+            else:  # gloo rehearsal: the same exchange through host copies of the rows it moves
+                h_in, h_top, h_bot = host
+                for kind, _, first, n in mg.halo_plan(H, world, rank, O):
+                    if kind == "send":
+                        h_in[:, first:first + n].copy_(inp[:, first:first + n])
+                mg.exchange_halo(h_in, h_top, h_bot, H, world, rank, O, dist=dist)
+                top.copy_(h_top)
+                bot.copy_(h_bot)
+            ctxs[i].build_gaussian(st)
+
+        steps_fn = [lambda st, i=i: conv_step(i, st) for i in range(rotate)]
     elif args.op == "conv":
         steps_fn = [c.build_gaussian for c in ctxs]
     else:
@@ -507,6 +565,8 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
     wall, kernel_ms = mg.max_over_ranks([wall, kernel_ms], dist=dist, device=red_dev)
     parity = verify(ctx, cfg, args.config, world, rank, dist, mg, first_image) if args.op == "build" else None
+    if halo_exchange:
+        parity = verify_conv_bands(ctx, cfg, world, rank, dist, mg, args.input)
     if parity is not None and rotate > 1:
         # every rotated set built the same images: their checksums must all equal set 0's
         sums = {c.checksum(0) for c in ctxs}
@@ -569,10 +629,14 @@ def main():
                                  if ctx.tuning()["conv_kernel"] == 0 and S <= 3 else
                                  "k_conv (extension: separable Gaussian convolution, LDS halo tiles)")}[args.op]),
             "kernel_ms": round(kernel_ms, 6),
+            **({"step_includes": "halo exchange (distributed.exchange_halo, RCCL point-to-point) before each band build"}
+               if halo_exchange else {}),
             "algorithmic_bytes_per_launch": bytes_launch,
         },
     }
-    result["parity"] = parity if args.op == "build" else {"status": "not checked for in-place re-entry ops"}
+    result["parity"] = parity if (args.op == "build" or halo_exchange) else (
+        {"status": "extension: no reference output (tests/ check it against a float64 convolution)"}
+        if args.op == "conv" else {"status": "not checked for in-place re-entry ops"})
     if distribution is not None:
         result["distribution"] = distribution
     if args.op != "build":

@@ -139,10 +139,26 @@ int gdp_generate_dog(gdp_ctx* ctx, void* stream);
  * NOT the reference's algorithm (which multiplies by a window, :119-131) and carries no parity
  * claim: G_s = base_o (*) k_s, the separable Gaussian with sigma_s = 2/(s+1) (the reference's
  * schedule), normalised taps over radius ceil(3 sigma_s) (<= 6), clamp-to-edge borders; same octave
- * bases, DoG and level layout as gdp_build.  Whole-image contexts only (a band has no halo rows).
+ * bases, DoG and level layout as gdp_build.  Row bands need their halo rows (below).
  * gdp_conv_taps returns scale s's 13 taps (zero beyond 2R+1) and radius R. */
 int gdp_build_gaussian(gdp_ctx* ctx, void* stream);
 int gdp_conv_taps(int S, int scale, float* taps13, int* radius);
+/* Row bands (multi-GPU split of one image): unlike the reference's
+ * pointwise window, the convolution reads 6 rows of every octave beyond a band's own rows, i.e.
+ * up to 6 * 2^(octaves-1) input rows above and below it (clipped to the image): *above / *below
+ * (0 for whole-image contexts).  A band's gdp_build_gaussian reads them from halo buffers
+ * [batch][rows][pitch] (the context's input format): the context's own (gdp_input_halo allocates
+ * one on first call and returns its device address, for a neighbour's rows to be written into —
+ * gdp_comm_exchange_halo over RCCL, or any copy) or caller device memory (gdp_bind_input_halo,
+ * zero copy; pitch and image stride multiples of 4, rows 16-B aligned).  gdp_device_input returns
+ * the device address and pitch of image b's input rows (the context's own or a bound buffer), the
+ * rows a neighbour needs.  A band build fails with GDP_ERR_STATE until both halos it needs are
+ * set, and only the block-tile kernel (GDP_TUNE_CONV_KERNEL 2, S <= 3, width a multiple of
+ * 2^(octaves+1)) runs on bands; its output equals the whole image's rows bit for bit. */
+int gdp_conv_halo_rows(const gdp_ctx* ctx, int* above, int* below);
+int gdp_input_halo(gdp_ctx* ctx, int side /* 0 above, 1 below */, void** rows, size_t* pitch);
+int gdp_bind_input_halo(gdp_ctx* ctx, const void* above, const void* below, size_t pitch, size_t image_stride);
+int gdp_device_input(const gdp_ctx* ctx, int b, const void** rows, size_t* pitch);
 
 /* ---- output --------------------------------------------------------------------------------
  * The blocking copies below are ordered after work on the context's OWN stream; if a build was

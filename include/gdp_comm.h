@@ -64,6 +64,30 @@ const char* gdp_comm_last_error(const gdp_comm* comm); /* comm may be NULL: last
 int gdp_comm_gather_bands(gdp_comm* comm, gdp_ctx* band, int band_image, gdp_ctx* full, int full_image, int root,
                           void* stream);
 
+/* ---- halo exchange of the convolution extension on row bands (gdp_build_gaussian) ----------
+ * The one step of the path with a real exchange: a band's convolution reads up to 6 * 2^(O-1)
+ * input rows of each neighbouring band (gdp_conv_halo_rows).  Rank r sends its first rows to
+ * r - 1 (that band's "below" halo) and its last rows to r + 1 (its "above" halo), and receives
+ * its own two halos.  The reference's pointwise window needs no exchange.
+ * gdp_comm_halo_plan: the schedule on rank `rank` (pure host arithmetic; neighbours are the
+ * adjacent non-empty bands of gdp_band_rows; GDP_ERR_ARG when a band is thinner than the halo).
+ * SEND: rows [first_row, first_row + rows) of this band (band-local); RECV_ABOVE / RECV_BELOW:
+ * the whole halo buffer of that side.  Issue order: per neighbour (above, then below) the send
+ * then the receive. */
+enum { GDP_HALO_SEND = 0, GDP_HALO_RECV_ABOVE = 1, GDP_HALO_RECV_BELOW = 2 };
+typedef struct gdp_halo_transfer {
+    int kind, peer, first_row, rows;
+} gdp_halo_transfer;
+int gdp_comm_halo_plan(int height, int nranks, int rank, int octaves, gdp_halo_transfer* out, int capacity,
+                       int* count);
+/* Collective over the ranks holding bands: fills `band`'s own halo buffers (gdp_input_halo) with
+ * the neighbours' input rows for every image of the batch, RCCL point-to-point grouped in one
+ * ncclGroupStart/End.  `band` must be gdp_band_rows' band of this rank (NULL on a rank whose band
+ * is empty), its input pitch the width rounded up to 4 (the owned input, or a bound input of that
+ * pitch).  Stream-ordered on `stream` (NULL = the band's stream); returns when enqueued (the
+ * following gdp_build_gaussian on the same stream sees the rows). */
+int gdp_comm_exchange_halo(gdp_comm* comm, gdp_ctx* band, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,10 @@ SIGNATURES = {
     "gdp_build": (_c_int, [_p, _p]),
     "gdp_build_gaussian": (_c_int, [_p, _p]),
     "gdp_conv_taps": (_c_int, [_c_int, _c_int, _p, ctypes.POINTER(_c_int)]),
+    "gdp_conv_halo_rows": (_c_int, [_p, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
+    "gdp_input_halo": (_c_int, [_p, _c_int, _pp, ctypes.POINTER(_c_size)]),
+    "gdp_bind_input_halo": (_c_int, [_p, _p, _p, _c_size, _c_size]),
+    "gdp_device_input": (_c_int, [_p, _c_int, _pp, ctypes.POINTER(_c_size)]),
     "gdp_init": (_c_int, [_p, _p]),
     "gdp_gauss_octave": (_c_int, [_p, _c_int, _p]),
     "gdp_gauss_range": (_c_int, [_p, _c_int, _c_int, _p]),

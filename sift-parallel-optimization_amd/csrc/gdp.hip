@@ -88,6 +88,7 @@ struct gdp_ctx {
     Geom geom{};
     Geom* d_geom = nullptr;
     void* d_in_own = nullptr;     // context-owned input buffer (int32 or uint8 per geom.in_fmt)
+    void* d_halo_own[2] = {nullptr, nullptr}; // context-owned halo rows above / below a band (conv extension)
     const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
     float* d_taps = nullptr;
@@ -596,6 +597,8 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_geom) (void)hipFree(c->d_geom);
     if (c->d_taps) (void)hipFree(c->d_taps);
     if (c->d_in_own) (void)hipFree(c->d_in_own);
+    for (void* h : c->d_halo_own)
+        if (h) (void)hipFree(h);
     if (c->d_out_own) (void)hipFree(c->d_out_own);
     if (c->d_ctaps) (void)hipFree(c->d_ctaps);
     if (c->d_cradius) (void)hipFree(c->d_cradius);
@@ -739,6 +742,11 @@ int gdp_set_input_format(gdp_ctx* c, int fmt) try {
     GDP_HIP(c, hipFree(c->d_in_own));
     c->d_in_own = fresh;
     c->geom.in_fmt = fmt;
+    for (int side = 0; side < 2; ++side) { // halo rows follow the input format: re-created on next use
+        if (c->d_halo_own[side]) GDP_HIP(c, hipFree(c->d_halo_own[side]));
+        c->geom.halo_ptr[side] = nullptr;
+        c->d_halo_own[side] = nullptr;
+    }
     return bind_input(c, nullptr, 0, 0, fmt, "gdp_set_input_format");
 } GDP_ABI_CATCH(c)
 
@@ -772,11 +780,116 @@ int gdp_conv_taps(int S, int scale, float* taps, int* radius) try {
     return GDP_OK;
 } GDP_ABI_CATCH(nullptr)
 
+// ---- convolution extension on row bands: halo rows --------------------------------------------
+// A band's convolution reads 6 octave-o rows beyond its octave-o rows; with band edges multiples of
+// 2^(O-1) that is at most 6 * 2^(O-1) input rows above and below (clipped to the image).
+static void conv_halo_counts(const Geom& g, int* above, int* below) {
+    const int hh = kCvR << (g.O - 1);
+    *above = std::min(hh, g.in_row0);
+    *below = std::min(hh, g.H - (g.in_row0 + g.in_rows));
+}
+
+int gdp_conv_halo_rows(const gdp_ctx* c, int* above, int* below) try {
+    if (!c || !above || !below) return GDP_ERR_ARG;
+    conv_halo_counts(c->geom, above, below);
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+int gdp_input_halo(gdp_ctx* c, int side, void** rows, size_t* pitch) try {
+    if (!c || side < 0 || side > 1 || !rows || !pitch) return c ? c->status(GDP_ERR_ARG, "gdp_input_halo: bad argument") : GDP_ERR_ARG;
+    Geom& g = c->geom;
+    int n[2];
+    conv_halo_counts(g, &n[0], &n[1]);
+    *pitch = (size_t)c->in_pitch_own;
+    if (n[side] == 0) {  // nothing beyond the image edge
+        *rows = nullptr;
+        return GDP_OK;
+    }
+    GDP_HIP(c, hipSetDevice(c->device));
+    if (!c->d_halo_own[side]) {
+        const size_t bytes = (size_t)n[side] * (size_t)c->in_pitch_own * g.batch * in_elem_size(c);
+        hipError_t e = hipMalloc(&c->d_halo_own[side], bytes);
+        if (e != hipSuccess) {
+            c->d_halo_own[side] = nullptr;
+            return c->status(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, "hipMalloc(halo rows)");
+        }
+        GDP_HIP(c, hipMemset(c->d_halo_own[side], 0, bytes));
+    }
+    g.halo_ptr[side] = c->d_halo_own[side];
+    g.halo_rows[side] = n[side];
+    g.halo_pitch[side] = c->in_pitch_own;
+    g.halo_img_stride[side] = (long long)n[side] * c->in_pitch_own;
+    *rows = c->d_halo_own[side];
+    return upload_geom(c);
+} GDP_ABI_CATCH(c)
+
+int gdp_bind_input_halo(gdp_ctx* c, const void* above, const void* below, size_t pitch, size_t image_stride) try {
+    if (!c) return GDP_ERR_ARG;
+    Geom& g = c->geom;
+    int n[2];
+    conv_halo_counts(g, &n[0], &n[1]);
+    const void* p[2] = {above, below};
+    for (int side = 0; side < 2; ++side) {
+        if (!p[side] || n[side] == 0) continue;
+        if (pitch < (size_t)g.W || pitch % 4 || (g.batch > 1 && image_stride < pitch * (size_t)n[side]) ||
+            image_stride % 4 || (reinterpret_cast<uintptr_t>(p[side]) & (g.in_fmt == GDP_INPUT_U8 ? 3 : 15)))
+            return c->status(GDP_ERR_ARG, "gdp_bind_input_halo: pitch / image stride must be multiples of 4 "
+                                          "(>= width, >= rows x pitch) and the rows 16-B (uint8: 4-B) aligned");
+    }
+    for (int side = 0; side < 2; ++side) {
+        g.halo_ptr[side] = n[side] ? p[side] : nullptr;
+        g.halo_rows[side] = n[side];
+        g.halo_pitch[side] = (long long)pitch;
+        g.halo_img_stride[side] = (long long)(g.batch > 1 ? image_stride : pitch * (size_t)n[side]);
+    }
+    return upload_geom(c);
+} GDP_ABI_CATCH(c)
+
+int gdp_device_input(const gdp_ctx* c, int b, const void** rows, size_t* pitch) try {
+    if (!c || b < 0 || b >= c->geom.batch || !rows || !pitch) return GDP_ERR_ARG;
+    *rows = static_cast<const char*>(c->d_in) + (size_t)b * (size_t)c->geom.in_img_stride * in_elem_size(c);
+    *pitch = (size_t)c->geom.in_pitch;
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+// Every input row a band convolution launch can read lies in the band or its held halo rows.
+static int conv_band_check(gdp_ctx* c) {
+    const Geom& g = c->geom;
+    int n[2];
+    conv_halo_counts(g, &n[0], &n[1]);
+    for (int side = 0; side < 2; ++side)
+        if (n[side] > 0 && (!g.halo_ptr[side] || g.halo_rows[side] != n[side]))
+            return c->status(GDP_ERR_STATE, "gdp_build_gaussian: this row band needs its %d halo rows %s "
+                                            "(gdp_input_halo / gdp_bind_input_halo / gdp_comm_exchange_halo)",
+                             n[side], side ? "below" : "above");
+    const long long lo = (long long)g.in_row0 - n[0], hi = (long long)g.in_row0 + g.in_rows + n[1]; // held rows
+    for (int o = 0; o < g.O; ++o) {
+        const OctGeom& og = g.oct[o];
+        if (og.rows == 0) continue;
+        if (og.cols < 4 || og.cols % 4)
+            return c->status(GDP_ERR_ARG, "gdp_build_gaussian on a row band needs every octave width a multiple "
+                                          "of 4 (width a multiple of 2^(octaves+1))");
+        const long long Hg = g.H >> o;
+        const long long first = std::max(0ll, (long long)og.row0 - kCvR) << o;
+        const long long last = std::min(Hg - 1, (long long)og.row0 + og.rows - 1 + kCvR) << o;
+        if (first < lo || last >= hi)
+            return c->status(GDP_ERR_STATE, "gdp_build_gaussian: octave %d reads input rows [%lld, %lld] beyond the "
+                                            "held rows [%lld, %lld)", o, first, last, lo, hi);
+    }
+    return GDP_OK;
+}
+
 int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     const Geom& g = c->geom;
-    if (g.in_row0 != 0 || g.in_rows != g.H)
-        return c->status(GDP_ERR_STATE, "gdp_build_gaussian: row-band contexts are not supported (needs halo rows)");
+    const bool band = g.in_row0 != 0 || g.in_rows != g.H;
+    if (band) {  // row band: only the block tiles read halo rows (every octave through them)
+        if (c->conv_kernel != 2 || g.L < 3 || g.L > 6)
+            return c->status(GDP_ERR_STATE, "gdp_build_gaussian on a row band runs the block tiles only "
+                                            "(GDP_TUNE_CONV_KERNEL 2, S <= 3)");
+        const int rc = conv_band_check(c);
+        if (rc != GDP_OK) return rc;
+    }
     GDP_HIP(c, hipSetDevice(c->device));
     if (!c->d_ctaps) {
         std::vector<float> t((size_t)g.L * kCvMaxTaps);

@@ -78,6 +78,35 @@ std::vector<gdp_transfer> make_plan(int H, int W, int S, int O, int nranks, int 
     return plan;
 }
 
+// The halo exchange schedule (gdp_comm_halo_plan): rows a band's convolution reads beyond it are
+// 6 * 2^(O-1) clipped to the image (gdp_conv_halo_rows), exchanged with the adjacent bands.
+int halo_counts_side(int H, int O, int r0, int r1, int side) {
+    const int hh = 6 << (O - 1);
+    return side == 0 ? std::min(hh, r0) : std::min(hh, H - r1);
+}
+int make_halo_plan(int H, int nranks, int rank, int O, std::vector<gdp_halo_transfer>& plan) {
+    int r0 = 0, r1 = 0;
+    gdp_band_rows(H, nranks, rank, O, &r0, &r1);
+    if (r1 <= r0) return GDP_OK;
+    if (rank > 0 && r0 > 0) {
+        int p0 = 0, p1 = 0;
+        gdp_band_rows(H, nranks, rank - 1, O, &p0, &p1);
+        const int need = halo_counts_side(H, O, p0, p1, 1), mine = halo_counts_side(H, O, r0, r1, 0);
+        if (need > r1 - r0 || mine > p1 - p0) return GDP_ERR_ARG;
+        plan.push_back({GDP_HALO_SEND, rank - 1, 0, need});
+        plan.push_back({GDP_HALO_RECV_ABOVE, rank - 1, 0, mine});
+    }
+    if (r1 < H) {
+        int n0 = 0, n1 = 0;
+        gdp_band_rows(H, nranks, rank + 1, O, &n0, &n1);
+        const int need = halo_counts_side(H, O, n0, n1, 0), mine = halo_counts_side(H, O, r0, r1, 1);
+        if (need > r1 - r0 || mine > n1 - n0) return GDP_ERR_ARG;
+        plan.push_back({GDP_HALO_SEND, rank + 1, r1 - r0 - need, need});
+        plan.push_back({GDP_HALO_RECV_BELOW, rank + 1, 0, mine});
+    }
+    return GDP_OK;
+}
+
 int fail_nothrow(gdp_comm* c, int code, const char* m) noexcept {
     try {
         return fail(c, code, m);
@@ -209,6 +238,67 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
                                    (size_t)t.rows * t.cols * 4, hipMemcpyDeviceToDevice, st));
     }
     GDP_HIPC(c, hipStreamSynchronize(st));
+    return GDP_OK;
+} GDP_COMM_CATCH(c)
+
+int gdp_comm_halo_plan(int H, int nranks, int rank, int O, gdp_halo_transfer* out, int capacity, int* count) try {
+    if (H <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || O <= 0 || !count || capacity < 0 || (capacity > 0 && !out))
+        return fail(nullptr, GDP_ERR_ARG, "gdp_comm_halo_plan: bad argument");
+    std::vector<gdp_halo_transfer> plan;
+    if (make_halo_plan(H, nranks, rank, O, plan) != GDP_OK)
+        return fail(nullptr, GDP_ERR_ARG, "gdp_comm_halo_plan: a row band is thinner than the halo");
+    *count = (int)plan.size();
+    if ((int)plan.size() > capacity) return fail(nullptr, GDP_ERR_ARG, "gdp_comm_halo_plan: capacity too small");
+    std::copy(plan.begin(), plan.end(), out);
+    return GDP_OK;
+} GDP_COMM_CATCH(nullptr)
+
+int gdp_comm_exchange_halo(gdp_comm* c, gdp_ctx* band, void* stream) try {
+    if (!c) return GDP_ERR_ARG;
+    if (!band) return GDP_OK;  // empty band: its neighbours do not count it as one
+    int H, W, S, O, B;
+    if (gdp_get_geometry(band, &H, &W, &S, &O, &B) != GDP_OK) return fail(c, GDP_ERR_ARG, "band geometry");
+    int r0 = 0, r1 = 0, rows0, cols0, first0;
+    gdp_band_rows(H, c->nranks, c->rank, O, &r0, &r1);
+    gdp_level_dims(band, 0, &rows0, &cols0, &first0);
+    if (first0 != r0 || rows0 != r1 - r0) return fail(c, GDP_ERR_ARG, "band context rows differ from gdp_band_rows' band of this rank");
+    std::vector<gdp_halo_transfer> plan;
+    if (make_halo_plan(H, c->nranks, c->rank, O, plan) != GDP_OK)
+        return fail(c, GDP_ERR_ARG, "a row band is thinner than the convolution halo");
+    const bool u8 = gdp_get_input_format(band) == GDP_INPUT_U8;
+    const size_t esz = u8 ? 1 : 4;
+    void* halo[2] = {nullptr, nullptr};
+    size_t hpitch[2] = {0, 0};
+    for (int side = 0; side < 2; ++side)
+        if (gdp_input_halo(band, side, &halo[side], &hpitch[side]) != GDP_OK) return fail(c, GDP_ERR_NOMEM, gdp_last_error(band));
+    int na = 0, nb = 0;
+    gdp_conv_halo_rows(band, &na, &nb);
+    GDP_HIPC(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)gdp_stream(band);
+    std::vector<std::pair<const void*, size_t>> inputs((size_t)B);
+    for (int b = 0; b < B; ++b) {
+        gdp_device_input(band, b, &inputs[(size_t)b].first, &inputs[(size_t)b].second);
+        if (inputs[(size_t)b].second != hpitch[0])
+            return fail(c, GDP_ERR_ARG, "band input pitch differs from its halo rows' (bind an input of pitch round_up(W, 4))");
+    }
+    const ncclDataType_t ty = u8 ? ncclUint8 : ncclInt32;
+    GDP_NCCL(c, ncclGroupStart());
+    for (int b = 0; b < B; ++b) {
+        const char* in = static_cast<const char*>(inputs[(size_t)b].first);
+        const size_t pitch = inputs[(size_t)b].second;
+        for (const gdp_halo_transfer& t : plan) {
+            const size_t n = (size_t)t.rows * pitch;  // whole padded rows (the same pitch on both sides)
+            if (t.kind == GDP_HALO_SEND) {
+                GDP_NCCL(c, ncclSend(in + (size_t)t.first_row * pitch * esz, n, ty, t.peer, c->comm, st));
+            } else {
+                const int side = t.kind == GDP_HALO_RECV_ABOVE ? 0 : 1;
+                const size_t rows_side = side ? (size_t)nb : (size_t)na;
+                GDP_NCCL(c, ncclRecv(static_cast<char*>(halo[side]) + (size_t)b * rows_side * hpitch[side] * esz, n, ty,
+                                     t.peer, c->comm, st));
+            }
+        }
+    }
+    GDP_NCCL(c, ncclGroupEnd());
     return GDP_OK;
 } GDP_COMM_CATCH(c)
 

@@ -16,6 +16,10 @@ Collectives appear only where the caller asks for a result on one rank:
   rank 0, receives each band's finished pyramid with one gather — the same result on the
   collector: the full pyramid, bit-identical to the serial reference.
 * `gather_checksums` — 8 bytes per image/band instead of the pyramids (verification at scale).
+* `exchange_halo` — the one real exchange step, and only for the true-Gaussian convolution
+  extension on row bands (gdp_build_gaussian): a convolution reads 6 rows of every octave beyond
+  a band, so each rank receives up to 6 * 2^(O-1) input rows from each neighbour (point-to-point,
+  RCCL over xGMI under "nccl") before its band build.  The reference's pointwise window needs none.
 
 The band/shard arithmetic and the assembly are pure torch / Python so the N > 1 logic runs under
 `gloo` on CPU in tests (tests/test_distributed.py) with the same code the GPU path uses.
@@ -52,6 +56,60 @@ def plan_band(H, world, rank, octaves):
     r0 = min(H, rank * per)
     r1 = min(H, (rank + 1) * per)
     return r0, r1
+
+
+def conv_halo_rows(H, octaves, r0, r1):
+    """(above, below) input rows a band [r0, r1)'s convolution reads beyond it: 6 * 2^(O-1)
+    clipped to the image (libgdp's gdp_conv_halo_rows)."""
+    hh = 6 << (int(octaves) - 1)
+    return min(hh, r0), min(hh, int(H) - r1)
+
+
+def halo_plan(H, world, rank, octaves):
+    """Point-to-point schedule of `exchange_halo` for `rank`: [(kind, peer, first_row, rows)], kind
+    "send" (rows of this band, band-local first row) or "recv_above" / "recv_below" (the whole
+    halo buffer).  Neighbours are the adjacent non-empty bands; a band thinner than the rows a
+    neighbour needs is an error (the halo would span several bands)."""
+    r0, r1 = plan_band(H, world, rank, octaves)
+    if r1 <= r0:
+        return []
+    ops = []
+    above, below = conv_halo_rows(H, octaves, r0, r1)
+    if rank > 0 and r0 > 0:  # rank - 1 owns the rows just above: it needs our first rows as its "below"
+        p0, p1 = plan_band(H, world, rank - 1, octaves)
+        need = conv_halo_rows(H, octaves, p0, p1)[1]
+        if need > r1 - r0 or above > p1 - p0:
+            raise ValueError(f"row bands of {r1 - r0} / {p1 - p0} rows are thinner than the {max(need, above)}-row halo")
+        ops.append(("send", rank - 1, 0, need))
+        ops.append(("recv_above", rank - 1, 0, above))
+    if r1 < H:
+        n0, n1 = plan_band(H, world, rank + 1, octaves)
+        need = conv_halo_rows(H, octaves, n0, n1)[0]
+        if need > r1 - r0 or below > n1 - n0:
+            raise ValueError(f"row bands of {r1 - r0} / {n1 - n0} rows are thinner than the {max(need, below)}-row halo")
+        ops.append(("send", rank + 1, r1 - r0 - need, need))
+        ops.append(("recv_below", rank + 1, 0, below))
+    return ops
+
+
+def exchange_halo(band, above, below, H, world, rank, octaves, dist=None):
+    """Fill this rank's halo buffers from its neighbours: `band` [B, rows, W] is this rank's input
+    band, `above` / `below` [B, n, W] receive the neighbours' rows (None when not needed).  Under
+    "nccl" the tensors are device tensors and the transfers are RCCL point-to-point over xGMI
+    (ordered after the current stream's work; the current stream waits for them); under "gloo"
+    they are CPU tensors.  One send/recv pair per neighbour and image."""
+    if dist is None or world == 1:
+        return
+    ops = []
+    for kind, peer, first, rows in halo_plan(H, world, rank, octaves):
+        for b in range(band.shape[0]):
+            if kind == "send":
+                ops.append(dist.P2POp(dist.isend, band[b, first:first + rows].contiguous(), peer))
+            else:
+                ops.append(dist.P2POp(dist.irecv, (above if kind == "recv_above" else below)[b], peer))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
 
 
 def band_level_rows(H, octaves, r0, r1):

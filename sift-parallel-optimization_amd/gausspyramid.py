@@ -160,6 +160,36 @@ class PyramidContext:
         check(lib().gdp_set_input_device(self._ctx, None, 0, 0), self._ctx)
         self._bound = None
 
+    # ------------------------------------------------------------------ row-band halos (conv extension)
+    def conv_halo_rows(self):
+        """(above, below): input rows a band's build_gaussian reads beyond its own rows."""
+        a, b = _i(), _i()
+        check(lib().gdp_conv_halo_rows(self._ctx, ctypes.byref(a), ctypes.byref(b)), self._ctx)
+        return a.value, b.value
+
+    def bind_input_halo(self, above=None, below=None, pitch=None, image_stride=None, keepalive=None):
+        """Read the halo rows from caller device memory (device pointers, [batch][rows][pitch] in
+        the input format; pitch defaults to the width)."""
+        pitch = self.W if pitch is None else int(pitch)
+        na, nb = self.conv_halo_rows()
+        stride = pitch * max(na, nb, 1) if image_stride is None else int(image_stride)
+        check(lib().gdp_bind_input_halo(self._ctx, ctypes.c_void_p(above or 0) if above else None,
+                                        ctypes.c_void_p(below or 0) if below else None, pitch, stride), self._ctx)
+        self._halo_keepalive = keepalive
+
+    def input_halo(self, side):
+        """(device address, pitch) of the context's own halo buffer (side 0 above, 1 below),
+        allocated on first call and used by the next band builds; (None, pitch) when none is needed."""
+        ptr, pitch = ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib().gdp_input_halo(self._ctx, int(side), ctypes.byref(ptr), ctypes.byref(pitch)), self._ctx)
+        return ptr.value, pitch.value
+
+    def device_input(self, b=0):
+        """(device address, pitch) of image b's input rows (own buffer or the bound one)."""
+        ptr, pitch = ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib().gdp_device_input(self._ctx, int(b), ctypes.byref(ptr), ctypes.byref(pitch)), self._ctx)
+        return ptr.value, pitch.value
+
     def fill_synthetic(self, seed=0x5EED, first_image=0, stream=None):
         check(lib().gdp_fill_synthetic(self._ctx, int(seed) & 0xFFFFFFFF, int(first_image), _stream_handle(stream)),
               self._ctx)

@@ -160,3 +160,104 @@ def test_checksum_restatement_is_order_independent(oracle):
             for s in range(S + 3):
                 parts = (parts + oracle.level_checksum(lv[(o, s)][a:b], o, s, a)) & 0xFFFFFFFFFFFFFFFF
     assert parts == whole
+
+
+# ---- halo exchange of the convolution extension on row bands ---------------------------------
+@pytest.mark.parametrize("H,O,world", [(16384, 5, 8), (4096, 5, 3), (1080, 5, 4), (512, 4, 2), (300, 3, 5)])
+def test_halo_plan_pairs_sends_with_receives(pkg, H, O, world):
+    """distributed.halo_plan (what exchange_halo executes): each band's received halo rows are
+    exactly its neighbours' rows above / below it (conv_halo_rows of the band), every send has the
+    neighbour's matching receive of the same size, and empty bands take no part."""
+    d = _dist_mod(pkg)
+    plans = {r: d.halo_plan(H, world, r, O) for r in range(world)}
+    bands = [d.plan_band(H, world, r, O) for r in range(world)]
+    for r, ops in plans.items():
+        r0, r1 = bands[r]
+        if r1 <= r0:
+            assert ops == []
+            continue
+        above, below = d.conv_halo_rows(H, O, r0, r1)
+        recv = {k: (p, n) for k, p, _, n in ops if k.startswith("recv")}
+        assert ("recv_above" in recv) == (above > 0) and ("recv_below" in recv) == (below > 0)
+        for kind, peer, first, rows in ops:
+            p0, p1 = bands[peer]
+            if kind == "send":  # the neighbour receives exactly these global rows
+                g0 = r0 + first
+                mine = [o for o in plans[peer] if o[0].startswith("recv") and o[1] == r]
+                assert len(mine) == 1 and mine[0][3] == rows
+                if peer == r - 1:  # its halo below = rows [p1, p1 + n)
+                    assert mine[0][0] == "recv_below" and g0 == p1
+                else:               # its halo above = rows [p0 - n, p0)
+                    assert mine[0][0] == "recv_above" and g0 + rows == p0
+            elif kind == "recv_above":
+                assert peer == r - 1 and rows == above and p1 == r0
+            else:
+                assert peer == r + 1 and rows == below and p0 == r1
+
+
+def test_halo_plan_matches_the_rccl_plan(pkg):
+    """gdp_comm_halo_plan (the C++ RCCL exchange's schedule) == distributed.halo_plan."""
+    import ctypes
+
+    class _Halo(ctypes.Structure):
+        _fields_ = [(f, ctypes.c_int) for f in ("kind", "peer", "first_row", "rows")]
+
+    pkg.lib()
+    L = ctypes.CDLL(os.path.join(REPO, "sift-parallel-optimization_amd", "lib", "libgdp_comm.so"))
+    d = _dist_mod(pkg)
+    kinds = {0: "send", 1: "recv_above", 2: "recv_below"}
+    for H, O, world in [(16384, 5, 8), (4096, 5, 3), (1080, 5, 4), (300, 3, 5), (4096, 13, 2)]:
+        for r in range(world):
+            count = ctypes.c_int()
+            buf = (_Halo * 8)()
+            assert L.gdp_comm_halo_plan(H, world, r, O, buf, 8, ctypes.byref(count)) == 0
+            got = [(kinds[buf[i].kind], buf[i].peer, buf[i].first_row, buf[i].rows) for i in range(count.value)]
+            assert got == d.halo_plan(H, world, r, O), (H, O, world, r)
+    # a band thinner than the halo: 4 x 16-row bands of a 64-row image need 96 halo rows at O = 5
+    assert L.gdp_comm_halo_plan(64, 4, 1, 5, buf, 8, ctypes.byref(count)) != 0
+    with pytest.raises(ValueError):
+        d.halo_plan(64, 4, 1, 5)
+
+
+def _halo_worker(rank, world, port, H, W, O, B, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, REPO)
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    d = __import__(pkg.__name__ + ".distributed", fromlist=["x"])
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        full = torch.arange(B * H * W, dtype=torch.int32).reshape(B, H, W)
+        r0, r1 = d.plan_band(H, world, rank, O)
+        above, below = d.conv_halo_rows(H, O, r0, r1)
+        band = full[:, r0:r1].contiguous()
+        top = torch.full((B, above, W), -1, dtype=torch.int32)
+        bot = torch.full((B, below, W), -1, dtype=torch.int32)
+        d.exchange_halo(band, top, bot, H, world, rank, O, dist=dist)
+        ok = torch.equal(top, full[:, r0 - above:r0]) and torch.equal(bot, full[:, r1:r1 + below])
+        q.put((rank, bool(ok), above, below))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W,O,B,world", [(512, 24, 4, 2, 2), (1080, 16, 5, 1, 3)])
+def test_exchange_halo_over_gloo(pkg, H, W, O, B, world):
+    """exchange_halo (RCCL point-to-point on GPUs) on gloo ranks: every band receives exactly the
+    rows above and below it that its convolution reads, for every image of the batch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, H, W, O, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in results), results
+    assert results[0][2] == 0 and results[-1][3] == 0 and any(a > 0 for _, _, a, _ in results)

@@ -826,3 +826,109 @@ def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt, batch
                 assert got.shape == ref.shape
                 err = np.abs(got - ref) - (1e-3 + 1e-5 * np.abs(ref))
                 assert err.max() <= 0, ((b, o, s), float(np.abs(got - ref).max()))
+
+
+def _hip_memcpy_h2d(dst, src_np):
+    """hipMemcpy into a raw device address (the context's own halo buffer) — test plumbing."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(dst, src_np.ctypes.data, src_np.nbytes, 1) == 0  # hipMemcpyHostToDevice (synchronous)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,O,nb,fmt,batch,owned", [(1024, 512, 5, 4, "i32", 1, False), (600, 256, 4, 3, "u8", 2, False),
+                                                      (1000, 384, 5, 2, "i32", 2, True), (512, 128, 3, 5, "i32", 1, True)])
+def test_conv_row_bands_with_halo_equal_whole_image(pkg, oracle, H, W, O, nb, fmt, batch, owned):
+    """Extension on row bands (the multi-GPU split of config 5): each band's gdp_build_gaussian,
+    given the halo rows above / below it (gdp_conv_halo_rows: 6 * 2^(O-1) input rows, clipped),
+    equals the whole image's build on its rows BIT FOR BIT, every octave and scale — through caller
+    device memory (gdp_bind_input_halo) and through the context's own halo buffers (gdp_input_halo,
+    what gdp_comm_exchange_halo receives into); batches and uint8 input.  Without its halos a band
+    build fails loudly."""
+    import importlib
+
+    import torch
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    dt = np.uint8 if fmt == "u8" else np.int32
+    imgs = [oracle.lcg_image(H, W, 31 + b).astype(dt) for b in range(batch)]
+    with pkg.PyramidContext(H, W, S=2, octaves=O, batch=batch, input_format=fmt) as whole:
+        for b, im in enumerate(imgs):
+            whole.set_input(im, b)
+        whole.build_gaussian()
+        whole.sync()
+        want = {(b, o, s): whole.level(b, o, s) for b in range(batch) for o in range(O) for s in range(5)}
+    for r in range(nb):
+        r0, r1 = d.plan_band(H, nb, r, O)
+        if r1 <= r0:
+            continue
+        with pkg.PyramidContext(H, W, S=2, octaves=O, batch=batch, row_begin=r0, row_end=r1, input_format=fmt) as ctx:
+            for b, im in enumerate(imgs):
+                ctx.set_input(np.ascontiguousarray(im[r0:r1]), b)
+            above, below = ctx.conv_halo_rows()
+            assert (above, below) == d.conv_halo_rows(H, O, r0, r1)
+            if above or below:
+                with pytest.raises(pkg.GdpError):
+                    ctx.build_gaussian()
+            rows = max(above, below, 1)
+            halo = [np.zeros((batch, rows, W), dtype=dt) for _ in range(2)]
+            for b, im in enumerate(imgs):
+                halo[0][b, :above] = im[r0 - above:r0]
+                halo[1][b, :below] = im[r1:r1 + below]
+            if owned:
+                for side, n in ((0, above), (1, below)):
+                    ptr, pitch = ctx.input_halo(side)
+                    assert (ptr is None) == (n == 0)
+                    if n:
+                        buf = np.zeros((batch, n, pitch), dtype=dt)
+                        buf[:, :, :W] = halo[side][:, :n]
+                        _hip_memcpy_h2d(ptr, buf)
+            else:
+                dev = [torch.from_numpy(h).cuda() for h in halo]
+                ctx.bind_input_halo(dev[0].data_ptr() if above else None, dev[1].data_ptr() if below else None,
+                                    pitch=W, image_stride=rows * W, keepalive=dev)
+            ctx.build_gaussian()
+            ctx.sync()
+            for b in range(batch):
+                for o in range(O):
+                    nrows, cols, first = ctx.level_dims(o)
+                    for s in range(5):
+                        got = ctx.level(b, o, s)
+                        ref = want[(b, o, s)][first:first + nrows]
+                        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (r, b, o, s)
+
+
+@pytest.mark.gpu
+def test_conv_config5_bands_checksums(pkg):
+    """Config 5 in the convolution mode: 8 row bands of 16384^2 (the 8-GPU split), halos bound from
+    the device-generated image, band checksums sum to the whole image's (bit-exact)."""
+    import importlib
+
+    import torch
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    H = W = 16384
+    O, nb = 5, 8
+    img = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    with pkg.PyramidContext(H, W, S=2, octaves=O, batch=1) as whole:
+        whole.bind_device_input(img.data_ptr(), W, H * W, keepalive=img)
+        whole.fill_synthetic(0x5EED, 0)
+        whole.build_gaussian()
+        whole.sync()
+        want = whole.checksum(0)
+    total = 0
+    for r in range(nb):
+        r0, r1 = d.plan_band(H, nb, r, O)
+        with pkg.PyramidContext(H, W, S=2, octaves=O, batch=1, row_begin=r0, row_end=r1) as ctx:
+            ctx.bind_device_input(img[r0:r1].data_ptr(), W, (r1 - r0) * W, keepalive=img)
+            above, below = ctx.conv_halo_rows()
+            top = img[r0 - above:r0].contiguous() if above else None
+            bot = img[r1:r1 + below].contiguous() if below else None
+            ctx.bind_input_halo(top.data_ptr() if above else None, bot.data_ptr() if below else None, pitch=W,
+                                keepalive=(top, bot))
+            ctx.build_gaussian()
+            ctx.sync()
+            total = (total + ctx.checksum(0)) & 0xFFFFFFFFFFFFFFFF
+    assert total == want
