@@ -472,7 +472,6 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
 
     // optional padding between levels (floats, multiple of 64) — layout experiment knob
     const char* pad_env = std::getenv("GDP_LEVEL_PAD");
-    if (const char* d = std::getenv("GDP_CONV_DIAG")) g.diag = std::atoi(d);
     const long long level_pad = pad_env ? round_up(std::max(0ll, std::atoll(pad_env)), kLevelAlign) : 0;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
     long long tap_off = 0, lev_off = 0, grp = 0;
@@ -904,6 +903,11 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     // the register sweep is compiled for S = 0..3 (L = 3..6) and takes the octaves whose width is a
     // multiple of 4; the LDS tiles take the rest (and everything for other S or conv_kernel = 1)
     const bool sweep = c->conv_kernel != 1 && g.L >= 3 && g.L <= 6;
+    {  // rows per tile / strip the selected kernel is instantiated for
+        const int r = c->conv_rows, k = c->conv_kernel;
+        const bool ok = k == 0 ? (r == 16 || r == 32) : true;
+        if (sweep && !ok) return c->status(GDP_ERR_STATE, "conv rows %d not available for conv kernel %d", r, k);
+    }
     const unsigned* blk = c->conv_kernel == 2 ? g.bk_blk : g.sw_blk;
     if (sweep && (c->conv_order & 4) && (c->conv_perm_dirty || c->conv_perm_kernel != c->conv_kernel)) {
         const int rc = conv_sweep_perm(c, blk);
