@@ -585,7 +585,9 @@ def main():
         bytes_launch = algorithmic_bytes(H, W, S, O, B, in_bytes)
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
     tun = ctx.tuning()
-    pmc = latest_pmc(args.config, tun["variant"], tun["tile_order"]) if args.op == "build" and args.input == "i32" else None
+    # PMC records are of the whole workload on one GPU: a row band (config 5 at N > 1) is another launch
+    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"])
+           if args.op == "build" and args.input == "i32" and not (cfg["band"] and world > 1) else None)
 
     result = {
         "metric": METRIC,
