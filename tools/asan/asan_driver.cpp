@@ -85,8 +85,26 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
         OK(gdp_build_gaussian(c, nullptr));
         OK(gdp_set_tuning(c, GDP_TUNE_CONV_KERNEL, 1));
         OK(gdp_build_gaussian(c, nullptr));
-    } else {
+    } else {  // row band: the convolution needs its halo rows first
+        int above = -1, below = -1;
+        OK(gdp_conv_halo_rows(c, &above, &below));
+        EXPECT(above >= 0 && below >= 0 && above + below > 0);
         EXPECT(gdp_build_gaussian(c, nullptr) != GDP_OK);
+        void* h[2] = {nullptr, nullptr};
+        size_t hp = 0;
+        for (int side = 0; side < 2; ++side) OK(gdp_input_halo(c, side, &h[side], &hp));
+        EXPECT(hp >= (size_t)W && (h[0] != nullptr) == (above > 0) && (h[1] != nullptr) == (below > 0));
+        EXPECT(gdp_input_halo(c, 2, &h[0], &hp) != GDP_OK);
+        EXPECT(gdp_bind_input_halo(c, h[0], h[1], (size_t)W + 1, 0) != GDP_OK || above + below == 0);  // pitch % 4
+        const void* in = nullptr;
+        size_t ip = 0;
+        OK(gdp_device_input(c, 0, &in, &ip));
+        EXPECT(in != nullptr && ip >= (size_t)W);
+        EXPECT(gdp_device_input(c, B, &in, &ip) != GDP_OK);
+        if (W % (1 << (go + 1)) == 0)
+            OK(gdp_build_gaussian(c, nullptr));  // every octave width a multiple of 4
+        else
+            EXPECT(gdp_build_gaussian(c, nullptr) != GDP_OK);
     }
     OK(gdp_fill_synthetic(c, 0x5EED, 3, nullptr));
     OK(gdp_set_input_format(c, GDP_INPUT_U8));
@@ -108,6 +126,7 @@ int main() {
     exercise(100, 37, 3, 0, 2, 0, 0);
     exercise(7, 5, 0, 0, 1, 0, 0);
     exercise(256, 300, 2, 5, 1, 16, 48);
+    exercise(512, 256, 2, 5, 2, 128, 256);
     exercise(1080, 1920, 2, 5, 1, 0, 0);
     gdp_ctx* c = nullptr;
     EXPECT(gdp_create(&c, 0, 10, 2, 0, 1, 0) != GDP_OK);
