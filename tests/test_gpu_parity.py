@@ -932,3 +932,33 @@ def test_conv_config5_bands_checksums(pkg):
             ctx.sync()
             total = (total + ctx.checksum(0)) & 0xFFFFFFFFFFFFFFFF
     assert total == want
+
+
+@pytest.mark.gpu
+def test_comm_exchange_halo_single_rank(pkg):
+    """gdp_comm_exchange_halo through RCCL on a one-rank communicator (the only RCCL world one GPU
+    allows): the whole image is the rank's band, the schedule is empty, and the call succeeds and
+    leaves the build unchanged; a context that is not gdp_band_rows' band of the rank is refused.
+    (Transfers between ranks need one GPU each: unmeasured here.)"""
+    import ctypes
+
+    pkg.lib()
+    L = ctypes.CDLL(os.path.join(os.path.dirname(pkg.__file__), "lib", "libgdp_comm.so"))
+    uid = (ctypes.c_ubyte * 128)()
+    assert L.gdp_comm_unique_id(uid) == 0
+    comm = ctypes.c_void_p()
+    assert L.gdp_comm_init(ctypes.byref(comm), uid, 1, 0, 0) == 0
+    try:
+        with pkg.PyramidContext(256, 256, S=2, octaves=5, batch=2) as ctx:
+            ctx.fill_synthetic(0x5EED, 0)
+            ctx.build_gaussian()
+            ctx.sync()
+            before = [ctx.checksum(b) for b in range(2)]
+            assert L.gdp_comm_exchange_halo(comm, ctx._ctx, None) == 0
+            ctx.build_gaussian()
+            ctx.sync()
+            assert [ctx.checksum(b) for b in range(2)] == before
+        with pkg.PyramidContext(256, 256, S=2, octaves=5, batch=1, row_begin=0, row_end=128) as band:
+            assert L.gdp_comm_exchange_halo(comm, band._ctx, None) != 0
+    finally:
+        L.gdp_comm_destroy(comm)
