@@ -962,3 +962,17 @@ def test_comm_exchange_halo_single_rank(pkg):
             assert L.gdp_comm_exchange_halo(comm, band._ctx, None) != 0
     finally:
         L.gdp_comm_destroy(comm)
+
+
+def test_cpp_conv_bands_mpi_example():
+    """examples/conv_bands_mpi (MPI launcher + RCCL halo exchange + banded gdp_build_gaussian) as
+    an MPI singleton and under mpiexec -n 1: the band checksums equal the whole image's."""
+    exe = os.path.join(REPO, "examples", "conv_bands_mpi")
+    if not os.path.exists(exe):
+        pytest.skip("examples/conv_bands_mpi not built (no MPI headers at build time)")
+    cmds = [[exe, "1024", "2"]]
+    if os.path.exists("/opt/conda/bin/mpiexec"):
+        cmds.append(["/opt/conda/bin/mpiexec", "-n", "1", exe, "4096", "2"])
+    for cmd in cmds:
+        r = subprocess.run(cmd, timeout=120, capture_output=True, text=True)
+        assert r.returncode == 0 and "bands == whole image" in r.stdout, (cmd, r.stdout, r.stderr)
