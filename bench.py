@@ -145,6 +145,25 @@ def cpu_baseline(budget_s):
                       f"median of {len(times)} calls", "cpu": cpu_info()}
 
 
+def latest_conv_pmc(config_key, tun):
+    """PMC record of the convolution extension's kernel on this workload with the run's conv
+    kernel / rows / order (profiles/pmc_<cfg>_conv*_*.json), or None."""
+    pdir = os.path.join(REPO, "profiles")
+    best = None
+    for f in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
+        if f.startswith("pmc_") and f.endswith(".json"):
+            try:
+                with open(os.path.join(pdir, f)) as fh:
+                    rec = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if rec.get("config") == config_key and rec.get("op") == "conv" and rec.get("kernel_bytes_per_launch") and \
+                    (rec.get("conv_kernel"), rec.get("conv_rows"), rec.get("conv_order")) == \
+                    (tun["conv_kernel"], tun["conv_rows"], tun["conv_order"]):
+                best = dict(rec, file=f)
+    return best
+
+
 def latest_pmc(config_key, variant, tile_order):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
@@ -588,6 +607,8 @@ def main():
     # PMC records are of the whole workload on one GPU: a row band (config 5 at N > 1) is another launch
     pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"])
            if args.op == "build" and args.input == "i32" and not (cfg["band"] and world > 1) else None)
+    if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
+        pmc = latest_conv_pmc(args.config, tun)
 
     result = {
         "metric": METRIC,
@@ -616,7 +637,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(pmc["kernel_bytes_per_launch"]) if pmc else None,
             "traffic_source": (f"profiles/{pmc['file']}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same "
-                               f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}) on this workload"
+                               + (f"kernel instance (conv kernel {pmc['conv_kernel']}, rows {pmc['conv_rows']}, order "
+                                  f"{pmc['conv_order']}) on this workload" if args.op == "conv" else
+                                  f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}) on this workload")
                                if pmc else "no PMC profile of this kernel instance (variant/tile order) on this workload"),
             "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d%s"
                        % (ctx.tuning()["variant"], ctx.tuning()["tile_order"], " (autotuned)" if autotuned else "")

@@ -104,3 +104,21 @@ def test_bench_refuses_more_nccl_ranks_than_gpus():
     r = _run_bench({"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "GDP_BENCH_BACKEND": "nccl"},
                    "--gpus", "2", "--no-cpu")
     assert r.returncode != 0 and "need 2 GPUs" in r.stderr
+
+
+def test_traffic_records_match_only_their_kernel_instance():
+    """roofline.traffic comes only from a PMC record of the same kernel instance: every build
+    variant x tile order the autotune can pick has one on every config, and the convolution record
+    is keyed by its conv kernel / rows / order."""
+    import bench
+
+    for cfg in ("c2", "c3", "c4", "c5"):
+        for v in range(19):
+            for t in (0, 1):
+                rec = bench.latest_pmc(cfg, v, t)
+                assert rec is not None and rec["variant"] == v and rec["tile_order"] == t, (cfg, v, t)
+                assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
+    assert bench.latest_pmc("c2", 99, 0) is None
+    conv = bench.latest_conv_pmc("c2", {"conv_kernel": 2, "conv_rows": 32, "conv_order": 4})
+    assert conv is not None and conv["op"] == "conv"
+    assert bench.latest_conv_pmc("c2", {"conv_kernel": 0, "conv_rows": 16, "conv_order": 0}) is None
