@@ -976,3 +976,45 @@ def test_cpp_conv_bands_mpi_example():
     for cmd in cmds:
         r = subprocess.run(cmd, timeout=120, capture_output=True, text=True)
         assert r.returncode == 0 and "bands == whole image" in r.stdout, (cmd, r.stdout, r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["i32", "u8"])
+def test_conv_row_band_unaligned_bound_input(pkg, oracle, fmt):
+    """A row band whose input is caller device memory with a pitch that is not a multiple of 4
+    (so octave 0 takes the scalar staging path) and halo rows in the context's own buffers:
+    still the whole image's rows bit for bit."""
+    import importlib
+
+    import torch
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    H, W, O = 640, 256, 4
+    dt, tdt = (np.uint8, torch.uint8) if fmt == "u8" else (np.int32, torch.int32)
+    img = oracle.lcg_image(H, W, 77).astype(dt)
+    with pkg.PyramidContext(H, W, S=2, octaves=O, batch=1, input_format=fmt) as whole:
+        whole.set_input(img)
+        whole.build_gaussian()
+        whole.sync()
+        want = {(o, s): whole.level(0, o, s) for o in range(O) for s in range(5)}
+    r0, r1 = d.plan_band(H, 3, 1, O)
+    pitch = W + 1
+    padded = np.zeros((r1 - r0, pitch), dtype=dt)
+    padded[:, :W] = img[r0:r1]
+    dev = torch.from_numpy(padded).cuda()
+    with pkg.PyramidContext(H, W, S=2, octaves=O, batch=1, row_begin=r0, row_end=r1, input_format=fmt) as ctx:
+        ctx.bind_device_input(dev.data_ptr(), pitch, (r1 - r0) * pitch, keepalive=dev)
+        above, below = ctx.conv_halo_rows()
+        assert above > 0 and below > 0
+        for side, rows in ((0, img[r0 - above:r0]), (1, img[r1:r1 + below])):
+            ptr, hp = ctx.input_halo(side)
+            buf = np.zeros((rows.shape[0], hp), dtype=dt)
+            buf[:, :W] = rows
+            _hip_memcpy_h2d(ptr, buf)
+        ctx.build_gaussian()
+        ctx.sync()
+        for o in range(O):
+            nrows, cols, first = ctx.level_dims(o)
+            for s in range(5):
+                got = ctx.level(0, o, s)
+                assert np.array_equal(got.view(np.uint32), want[(o, s)][first:first + nrows].view(np.uint32)), (o, s)
