@@ -93,3 +93,101 @@ def test_randomized_parity_sweep(pkg, oracle):
                 assert got.shape == wants[b].shape, what
                 bad = np.flatnonzero(_bits(got) != _bits(wants[b]))
                 assert bad.size == 0, (what, b, bad[:5])
+
+
+# ---- the convolution extension (no reference counterpart) -------------------------------------
+N_CONV_CASES = 120
+_CONV_TUNES = [dict(conv_kernel=2, conv_rows=32, conv_order=4), dict(conv_kernel=2, conv_rows=16, conv_order=0),
+               dict(conv_kernel=2, conv_rows=48, conv_order=5), dict(conv_kernel=2, conv_rows=24, conv_waves=8, conv_order=1),
+               dict(conv_kernel=2, conv_rows=8, conv_order=4), dict(conv_kernel=0, conv_rows=16, conv_order=5),
+               dict(conv_kernel=0, conv_rows=32, conv_order=2), dict(conv_kernel=1)]
+
+
+def _conv_ref(pkg, img, S, O):
+    """float64 separable convolution with the library's taps, clamp-to-edge (tests/test_gpu_parity.py)."""
+    H, W = img.shape
+    out = {}
+    for o in range(O):
+        base = img[:: 1 << o, :: 1 << o][: H >> o, : W >> o].astype(np.float64)
+        G = []
+        for s in range(S + 3):
+            k, R = pkg.conv_taps(S, s)
+            k = k.astype(np.float64)
+            p = np.pad(base, R, mode="edge")
+            h = sum(k[d] * p[:, d:d + base.shape[1]] for d in range(2 * R + 1))
+            G.append(sum(k[d] * h[d:d + base.shape[0]] for d in range(2 * R + 1)))
+        for s in range(S + 3):
+            out[(o, s)] = G[s] - G[s + 1] if s < S + 2 else G[s]
+    return out
+
+
+def test_randomized_convolution_sweep(pkg, oracle):
+    """Seeded sweep of the convolution extension: shape 1..400 x 1..400, S 0..4, octave count,
+    batch, int32 / uint8, every kernel / rows / waves / order the library has, against a float64
+    convolution within the stated tolerance |err| <= 1e-3 + 1e-5 |ref|; and, when the width allows
+    (a multiple of 2^(O+1), S <= 3), a random row-band split whose bands — given their halo rows —
+    equal the whole image's build bit for bit."""
+    import importlib
+
+    import torch
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    rng = np.random.default_rng(20261017)
+    for i in range(N_CONV_CASES):
+        H = int(rng.integers(1, 401))
+        W = int(rng.integers(1, 401)) if rng.random() < 0.6 else int(rng.integers(1, 13)) * 32
+        S = int(rng.integers(0, 5))
+        omax = max(1, int(np.floor(np.log2(min(H, W)))) + 1)
+        O = int(rng.integers(1, min(omax, 6) + 1))
+        B = int(rng.integers(1, 3))
+        fmt = "u8" if rng.random() < 0.3 else "i32"
+        tune = _CONV_TUNES[int(rng.integers(0, len(_CONV_TUNES)))]
+        dt = np.uint8 if fmt == "u8" else np.int32
+        imgs = [rng.integers(0, 256, size=(H, W), dtype=np.int64).astype(dt) for _ in range(B)]
+        what = dict(case=i, H=H, W=W, S=S, O=O, B=B, fmt=fmt, tune=tune)
+        with pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, input_format=fmt) as ctx:
+            ctx.set_tuning(**tune)
+            for b, im in enumerate(imgs):
+                ctx.set_input(im, b)
+            ctx.build_gaussian()
+            ctx.sync()
+            whole = {(b, o, s): ctx.level(b, o, s) for b in range(B) for o in range(O) for s in range(S + 3)}
+        for b, im in enumerate(imgs):
+            for (o, s), ref in _conv_ref(pkg, im.astype(np.int32), S, O).items():
+                got = whole[(b, o, s)].astype(np.float64)
+                assert got.shape == ref.shape, what
+                assert (np.abs(got - ref) - (1e-3 + 1e-5 * np.abs(ref))).max() <= 0, (what, b, o, s)
+        align = 1 << (max(O, 5) - 1)
+        if S <= 3 and W % (1 << (O + 1)) == 0 and H > 2 * align and rng.random() < 0.6:
+            nb = int(rng.integers(2, max(3, H // align) + 1))
+            for r in range(nb):
+                r0, r1 = d.plan_band(H, nb, r, O)
+                if r1 <= r0:
+                    continue
+                try:
+                    plan_ok = True
+                    d.halo_plan(H, nb, r, O)
+                except ValueError:
+                    plan_ok = False  # bands thinner than the halo: a band context still works locally
+                with pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, row_begin=r0, row_end=r1, input_format=fmt) as bc:
+                    bc.set_tuning(conv_kernel=2, conv_rows=tune.get("conv_rows", 32) if tune.get("conv_kernel") == 2 else 32,
+                                  conv_waves=tune.get("conv_waves", 16))
+                    for b, im in enumerate(imgs):
+                        bc.set_input(np.ascontiguousarray(im[r0:r1]), b)
+                    above, below = bc.conv_halo_rows()
+                    rows = max(above, below, 1)
+                    halo = [np.zeros((B, rows, W), dtype=dt) for _ in range(2)]
+                    for b, im in enumerate(imgs):
+                        halo[0][b, :above] = im[r0 - above:r0]
+                        halo[1][b, :below] = im[r1:r1 + below]
+                    dev = [torch.from_numpy(h).cuda() for h in halo]
+                    bc.bind_input_halo(dev[0].data_ptr() if above else None, dev[1].data_ptr() if below else None,
+                                       pitch=W, image_stride=rows * W, keepalive=dev)
+                    bc.build_gaussian()
+                    bc.sync()
+                    for b in range(B):
+                        for o in range(O):
+                            n, _, first = bc.level_dims(o)
+                            for s in range(S + 3):
+                                assert np.array_equal(_bits(bc.level(b, o, s)), _bits(whole[(b, o, s)][first:first + n])), \
+                                    (what, "band", r, nb, plan_ok, b, o, s)
