@@ -253,7 +253,7 @@ enum {
     GDP_TUNE_STAGE_KB = 13,     /* row-pointer downloads: KiB per half of the double-buffered
                                    pinned staging buffer (32768 default) */
     GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
-                                   into the caller's rows (4 default) */
+                                   into the caller's rows (8 default, at most the host's threads) */
     GDP_TUNE_CONV_WAVES = 15    /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);

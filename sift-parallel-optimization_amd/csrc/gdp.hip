@@ -108,7 +108,9 @@ struct gdp_ctx {
     float* h_stage = nullptr;     // pinned staging for row-pointer downloads (two halves)
     size_t h_stage_floats = 0;
     size_t stage_half_floats = kStageFloats / 2; // GDP_TUNE_STAGE_KB
-    int stage_threads = 4;        // GDP_TUNE_STAGE_THREADS: host threads scattering a staged batch
+    int stage_threads = 8;        // GDP_TUNE_STAGE_THREADS: host threads scattering a staged batch (8: 4096^2
+                                  // pyramid download 8.77 vs 9.99 ms with 4, tools/mirror_bench.py; capped by
+                                  // the host's hardware threads at context creation)
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
     unsigned long long* d_sum = nullptr;
     std::vector<float> h_taps;
@@ -454,6 +456,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     c->conv_kernel = 2;
     c->conv_rows = 32;
     c->conv_order = 4;
+    {
+        const unsigned hw = std::thread::hardware_concurrency();
+        if (hw > 0) c->stage_threads = std::max(1, std::min<int>(c->stage_threads, (int)hw));
+    }
     Geom& g = c->geom;
     g.H = H;
     g.W = W;
