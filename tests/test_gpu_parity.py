@@ -1018,3 +1018,24 @@ def test_conv_row_band_unaligned_bound_input(pkg, oracle, fmt):
             for s in range(5):
                 got = ctx.level(0, o, s)
                 assert np.array_equal(got.view(np.uint32), want[(o, s)][first:first + nrows].view(np.uint32)), (o, s)
+
+
+def test_bench_selflaunched_ranks_certify_their_work():
+    """bench.py --gpus 2 started without a launcher (the driver's command form) on this one GPU,
+    ranks over gloo: the default build certifies both ranks' images bit-exact, and the banded
+    convolution (config 5) exchanges halo rows every step and certifies bands == whole image."""
+    import json
+
+    env = dict(os.environ, GDP_BENCH_BACKEND="gloo")
+    for args, key in ((["--steps", "5", "--warmup", "1", "--no-cpu", "--no-autotune"], "build"),
+                      (["--op", "conv", "--config", "c5", "--steps", "2", "--warmup", "1"], "conv")):
+        r = subprocess.run(["python3", os.path.join(REPO, "bench.py"), "--gpus", "2"] + args, env=env, timeout=240,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, (key, r.stderr[-2000:])
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        assert line["n_gpus"] == 2, key
+        if key == "build":
+            assert line["parity"]["status"] == "bit-exact" and line["parity"]["ranks_certified"] == [0, 1]
+        else:
+            assert line["parity"]["status"] == "bands == whole image (bit-exact)", line["parity"]
+            assert "halo exchange" in line["roofline"]["step_includes"]
