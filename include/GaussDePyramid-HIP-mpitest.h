@@ -39,6 +39,7 @@ int layer = 0;
 bool is_initialized = false;
 static gdp_ctx* gdp_mpitest_ctx = nullptr;
 static bool gdp_mpitest_fresh = false;
+static float* gdp_mpitest_host = nullptr;  // pinned device-layout mirror the GaussPy rows point into
 
 static inline void gdp_mpitest_check(int status, const char* what) {
     if (status != GDP_OK) {
@@ -47,26 +48,38 @@ static inline void gdp_mpitest_check(int status, const char* what) {
     }
 }
 
+static inline int gdp_mpitest_download() {
+    return gdp_mpitest_host ? gdp_download_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
+                            : gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy);
+}
+
 // :438-473 — first call allocates GaussPy (and the device context); every call refills.
 void GaussPyInit(int* data[MAX]) {
     length = n;
     if (!is_initialized) {
         layer = gdp_octaves_for(length);
+        gdp_mpitest_check(gdp_create(&gdp_mpitest_ctx, length, length, S, layer, 1, 0), "GaussPyInit");
+        gdp_mpitest_check(gdp_set_window_centre(gdp_mpitest_ctx, GDP_CENTRE_INTLEN), "GaussPyInit");
+        // the rows (one new float[] each in the reference) point into one pinned buffer in the
+        // device layout: every download is a single DMA copy (separate rows if pinning is refused)
+        void* h = nullptr;
+        gdp_mpitest_host = gdp_host_alloc(gdp_image_floats(gdp_mpitest_ctx) * sizeof(float), &h) == GDP_OK
+                               ? static_cast<float*>(h) : nullptr;
         GaussPy = new float***[layer];
         for (int o = 0; o < layer; ++o) {
             GaussPy[o] = new float**[S + 3];
             for (int s = 0; s < S + 3; ++s) {
                 GaussPy[o][s] = new float*[length >> o];
-                for (int r = 0; r < (length >> o); ++r) GaussPy[o][s][r] = new float[length >> o];
+                float* lev = gdp_mpitest_host ? gdp_mpitest_host + gdp_level_offset(gdp_mpitest_ctx, 0, o, s) : nullptr;
+                for (int r = 0; r < (length >> o); ++r)
+                    GaussPy[o][s][r] = lev ? lev + (size_t)r * (length >> o) : new float[length >> o];
             }
         }
-        gdp_mpitest_check(gdp_create(&gdp_mpitest_ctx, length, length, S, layer, 1, 0), "GaussPyInit");
-        gdp_mpitest_check(gdp_set_window_centre(gdp_mpitest_ctx, GDP_CENTRE_INTLEN), "GaussPyInit");
     }
     is_initialized = true;
     gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
     gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
-    gdp_mpitest_check(gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy), "GaussPyInit");
+    gdp_mpitest_check(gdp_mpitest_download(), "GaussPyInit");
     gdp_mpitest_fresh = true;
 }
 
@@ -76,7 +89,7 @@ static inline void gdp_mpitest_generate() {
                       "GenerateDoG_mpi");
     gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");
     gdp_mpitest_fresh = false;
-    gdp_mpitest_check(gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy), "GenerateDoG_mpi");
+    gdp_mpitest_check(gdp_mpitest_download(), "GenerateDoG_mpi");
     auto end = std::chrono::steady_clock::now();
     std::cout << std::chrono::duration<double>(end - begin).count() << std::endl;
 }
@@ -89,12 +102,15 @@ void delete_mpi() {
     if (!is_initialized) return;
     for (int o = 0; o < layer; ++o) {
         for (int s = 0; s < S + 3; ++s) {
-            for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
+            if (!gdp_mpitest_host)
+                for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
             delete[] GaussPy[o][s];
         }
         delete[] GaussPy[o];
     }
     delete[] GaussPy;
+    gdp_host_free(gdp_mpitest_host);
+    gdp_mpitest_host = nullptr;
     gdp_destroy(gdp_mpitest_ctx);
     gdp_mpitest_ctx = nullptr;
     is_initialized = false;

@@ -66,6 +66,8 @@ protected:
     float* filter;  // unused (taps live on the device); kept for layout parity with :28
     gdp_ctx* ctx_;
     bool fresh_;  // contents == GaussPyInit(): GenerateDoG may use the fused build kernel
+    float* host_; // pinned host pyramid in the device layout that the GaussPy rows point into
+                  // (gdp_host_alloc); NULL: rows are separate new[] arrays (pinned memory refused)
     static void check_(gdp_ctx* c, int status, const char* what) {
         if (status != GDP_OK) {
             std::fprintf(stderr, "GaussPyramid_hip::%s failed: %s (%s)\n", what, gdp_status_string(status),
@@ -77,11 +79,11 @@ protected:
 
 inline GaussPyramid_hip::GaussPyramid_hip()
     : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), length(0), S(0), layer(0),
-      filter(nullptr), ctx_(nullptr), fresh_(false) {}
+      filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {}
 
 inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device)
     : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), length(len), S(S_), layer(0),
-      filter(nullptr), ctx_(nullptr), fresh_(false) {
+      filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {
     data = new int*[len];
     for (int i = 0; i < len; ++i) {
         data[i] = new int[len];
@@ -91,20 +93,26 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
     filter = new float[len];
     check_(nullptr, gdp_create(&ctx_, len, len, S, layer, 1, device), "GaussPyramid_hip");
     check_(ctx_, gdp_set_input_rows(ctx_, 0, (const int32_t* const*)data, nullptr), "GaussPyramid_hip");
+    // The GaussPy rows (:16, one new float[] per row in the reference) point into ONE pinned host
+    // buffer laid out like the device pyramid, so SyncHost is a single DMA copy at the full PCIe
+    // rate; if pinned memory is refused, separate rows and the staged scatter are used instead.
+    void* h = nullptr;
+    if (gdp_host_alloc(gdp_image_floats(ctx_) * sizeof(float), &h) == GDP_OK) host_ = static_cast<float*>(h);
     GaussPy = new float***[layer];
     for (int o = 0; o < layer; ++o) {
         const int n = len >> o;
         GaussPy[o] = new float**[S + 3];
         for (int s = 0; s < S + 3; ++s) {
             GaussPy[o][s] = new float*[n];
-            for (int r = 0; r < n; ++r) GaussPy[o][s][r] = new float[n];
+            float* lev = host_ ? host_ + gdp_level_offset(ctx_, 0, o, s) : nullptr;
+            for (int r = 0; r < n; ++r) GaussPy[o][s][r] = lev ? lev + (size_t)r * n : new float[n];
         }
     }
     GaussPyInit();
 }
 
-inline void GaussPyramid_hip::SyncHost() {  // one staged copy + one sync per 64 MiB, not one per level
-    check_(ctx_, gdp_download_pyramid_rows(ctx_, 0, GaussPy), "SyncHost");
+inline void GaussPyramid_hip::SyncHost() {  // one DMA copy (pinned mirror) or one staged copy per 64 MiB
+    check_(ctx_, host_ ? gdp_download_image_raw(ctx_, 0, host_) : gdp_download_pyramid_rows(ctx_, 0, GaussPy), "SyncHost");
 }
 
 inline void GaussPyramid_hip::GaussPyInit() {
@@ -148,13 +156,15 @@ inline GaussPyramid_hip::~GaussPyramid_hip() {
     if (GaussPy) {
         for (int o = 0; o < layer; ++o) {
             for (int s = 0; s < S + 3; ++s) {
-                for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
+                if (!host_)
+                    for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
                 delete[] GaussPy[o][s];
             }
             delete[] GaussPy[o];
         }
         delete[] GaussPy;
     }
+    gdp_host_free(host_);
     if (data) {
         for (int i = 0; i < length; ++i) delete[] data[i];
         delete[] data;

@@ -192,6 +192,19 @@ size_t gdp_packed_floats(const gdp_ctx* ctx);
  * context's own buffer. */
 int gdp_set_output_device(gdp_ctx* ctx, float* base, size_t bytes);
 size_t gdp_level_offset(const gdp_ctx* ctx, int b, int octave, int scale);
+
+/* ---- host mirror in the device layout (the drop-in classes' fast path) ---------------------
+ * gdp_host_alloc: pinned (page-locked) host memory, which one DMA copy fills at the full PCIe
+ * rate (gdp_host_free releases it).  gdp_image_floats: floats of one image's pyramid in the device
+ * layout — level (o, s) at gdp_level_offset(ctx, 0, o, s), dense rows of cols_o floats, levels
+ * 256-B aligned.  gdp_download_image_raw: copy image b's pyramid in that layout to `host` in ONE
+ * D2H copy (blocking).  A caller that points the reference's float**** rows into such a buffer
+ * (GaussPy[o][s][r] = host + gdp_level_offset(ctx, 0, o, s) + r * cols_o) mirrors the device with
+ * no per-row scatter (include/GaussDePyramid-HIP.h does). */
+int gdp_host_alloc(size_t bytes, void** host);
+void gdp_host_free(void* host);
+size_t gdp_image_floats(const gdp_ctx* ctx);
+int gdp_download_image_raw(gdp_ctx* ctx, int b, float* host);
 /* Order-independent 64-bit checksum of image b's pyramid (blocking): the sum, mod 2^64, over
  * every word of every level of splitmix64_fin(idx * 0x9E3779B97F4A7C15 + (o*64+s) *
  * 0xD1B54A32D192ED03 + float_bits), idx = global_row * cols + col.  Row-band checksums add up

@@ -1194,6 +1194,33 @@ size_t gdp_level_offset(const gdp_ctx* c, int b, int o, int s) {
     return (size_t)b * c->geom.pyr_stride + og.lev_off + (size_t)s * og.lev_stride;
 }
 
+int gdp_host_alloc(size_t bytes, void** host) try {
+    if (!host || bytes == 0) return GDP_ERR_ARG;
+    *host = nullptr;
+    const hipError_t e = hipHostMalloc(host, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *host = nullptr;
+        return e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP;
+    }
+    return GDP_OK;
+} GDP_ABI_CATCH(nullptr)
+
+void gdp_host_free(void* host) {
+    if (host) (void)hipHostFree(host);
+}
+
+size_t gdp_image_floats(const gdp_ctx* c) { return c ? (size_t)c->geom.pyr_stride : 0; }
+
+int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_download_image_raw: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipMemcpyAsync(host, c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->geom.pyr_stride * 4,
+                              hipMemcpyDeviceToHost, c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
 int gdp_checksum(gdp_ctx* c, int b, uint64_t* out) try {
     if (!c || !out || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_checksum: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
