@@ -97,7 +97,12 @@ protected:
             std::abort();
         }
     }
-    void sync_host_() { check_(gdp_download_pyramid_rows(full_, 0, GaussPy), "download", full_); }
+    float* host_ = nullptr;  // pinned device-layout mirror the GaussPy rows point into (NULL: new[] rows)
+    void sync_host_() {
+        check_(host_ ? gdp_download_image_raw(full_, 0, host_) : gdp_download_pyramid_rows(full_, 0, GaussPy),
+               "download", full_);
+    }
+    void ensure_full_();
 };
 
 inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi()
@@ -115,12 +120,18 @@ inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi(int** img, int len, int S_) : 
     }
     layer = gdp_octaves_for(len);
     filter = new float[len];
+    ensure_full_();
+    // the rows (one new float[] each in the reference) point into one pinned buffer laid out like
+    // the device pyramid: the collector's mirror is a single DMA copy (new[] rows if refused)
+    void* h = nullptr;
+    if (gdp_host_alloc(gdp_image_floats(full_) * sizeof(float), &h) == GDP_OK) host_ = static_cast<float*>(h);
     GaussPy = new float***[layer];
     for (int o = 0; o < layer; ++o) {
         GaussPy[o] = new float**[S + 3];
         for (int s = 0; s < S + 3; ++s) {
             GaussPy[o][s] = new float*[len >> o];
-            for (int r = 0; r < (len >> o); ++r) GaussPy[o][s][r] = new float[len >> o];
+            float* lev = host_ ? host_ + gdp_level_offset(full_, 0, o, s) : nullptr;
+            for (int r = 0; r < (len >> o); ++r) GaussPy[o][s][r] = lev ? lev + (size_t)r * (len >> o) : new float[len >> o];
         }
     }
     GaussPyInit();
@@ -141,13 +152,16 @@ inline int gdp_launcher_rank() {
     return 0;
 }
 
+inline void GaussPyramid_hip_mpi::ensure_full_() {  // the whole-image context on this rank's GPU
+    if (full_) return;
+    const int ndev = gdp_device_count();
+    check_(gdp_create(&full_, length, length, S, layer, 1, ndev > 0 ? gdp_launcher_rank() % ndev : 0), "GaussPyInit",
+           nullptr);
+    check_(gdp_set_input_rows(full_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit", full_);
+}
+
 inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GPU)
-    if (!full_) {
-        const int ndev = gdp_device_count();
-        check_(gdp_create(&full_, length, length, S, layer, 1, ndev > 0 ? gdp_launcher_rank() % ndev : 0),
-               "GaussPyInit", nullptr);
-        check_(gdp_set_input_rows(full_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit", full_);
-    }
+    ensure_full_();
     check_(gdp_init(full_, nullptr), "GaussPyInit", full_);
     is_initialized = true;
     fresh_ = true;
@@ -229,13 +243,15 @@ inline GaussPyramid_hip_mpi::~GaussPyramid_hip_mpi() {
     if (GaussPy) {
         for (int o = 0; o < layer; ++o) {
             for (int s = 0; s < S + 3; ++s) {
-                for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
+                if (!host_)
+                    for (int r = 0; r < (length >> o); ++r) delete[] GaussPy[o][s][r];
                 delete[] GaussPy[o][s];
             }
             delete[] GaussPy[o];
         }
         delete[] GaussPy;
     }
+    gdp_host_free(host_);
     if (data) {
         for (int i = 0; i < length; ++i) delete[] data[i];
         delete[] data;
