@@ -261,3 +261,25 @@ def test_exchange_halo_over_gloo(pkg, H, W, O, B, world):
         assert p.exitcode == 0
     assert all(ok for _, ok, _, _ in results), results
     assert results[0][2] == 0 and results[-1][3] == 0 and any(a > 0 for _, _, a, _ in results)
+
+
+@pytest.mark.parametrize("H,O,world", [(16384, 5, 8), (4096, 5, 3), (1080, 5, 4), (512, 4, 2), (300, 3, 5), (4096, 9, 2),
+                                       (1000, 6, 3)])
+def test_halo_rows_cover_every_row_the_band_convolution_reads(pkg, H, O, world):
+    """The band convolution stages, for octave o, global octave-o rows [row0_o - 6, row0_o + rows_o
+    + 5] clamped to the image (row0_o = ceil(r0 / 2^o), rows_o the band's octave-o rows), i.e.
+    input rows (r << o): conv_halo_rows' 6 * 2^(O-1) rows above / below cover all of them (what
+    gdp_build_gaussian's host check enforces before launching)."""
+    d = _dist_mod(pkg)
+    for r in range(world):
+        r0, r1 = d.plan_band(H, world, r, O)
+        if r1 <= r0:
+            continue
+        above, below = d.conv_halo_rows(H, O, r0, r1)
+        for o, (first, rows) in enumerate(d.band_level_rows(H, O, r0, r1)):
+            if rows == 0:
+                continue
+            Hg = H >> o
+            lo = max(0, first - 6) << o
+            hi = min(Hg - 1, first + rows - 1 + 6) << o
+            assert r0 - above <= lo and hi < r1 + below, (H, O, world, r, o, lo, hi, r0 - above, r1 + below)
