@@ -279,6 +279,8 @@ def scatter_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
     H, W, B = cfg["H"], cfg["W"], cfg["batch"]
     dt = torch.uint8 if in_fmt == "u8" else torch.int32
     dev = torch.device("cuda", torch.cuda.current_device())
+    if cfg["band"]:
+        return scatter_band_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt, dt, dev)
     per = B * H * W
 
     def fill(chunk, r):  # the device generator writes straight into rank r's share
@@ -306,6 +308,115 @@ def scatter_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
     return {"mode": f"collective scatter of rank 0's batch ({'RCCL over xGMI' if backend == 'nccl' else backend + ' via host'}), "
                     "outside the timed region", "bytes": nbytes, "ms": round(secs * 1e3, 3),
             "GBps": round(nbytes / secs / 1e9, 1) if secs > 0 else None, "bit_exact": bad == 0.0}
+
+
+def scatter_band_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt, dt, dev):
+    """The row-band config's input split (optional): rank 0 generates the whole
+    image and one collective scatter hands every rank its rows (padded to the largest band);
+    each rank builds its band from them and checks the pyramid checksum against its locally
+    generated band.  Outside the timed region."""
+    import torch
+
+    import __graft_entry__ as entry
+
+    H, W, O = cfg["H"], cfg["W"], cfg["O"]
+    bands = [mg.plan_band(H, world, r, O) for r in range(world)]
+    per = max(r1 - r0 for r0, r1 in bands) * W
+    whole_img = None
+    if rank == 0:
+        pkg = entry.load_package()
+        whole_img = torch.empty((H, W), dtype=dt, device=dev)
+        with pkg.PyramidContext(H, W, S=2, octaves=O, batch=1, device=ctx.device, input_format=in_fmt) as whole:
+            whole.bind_device_input(whole_img.data_ptr(), W, H * W, keepalive=whole_img)
+            whole.fill_synthetic(SEED, 0)
+            whole.sync()
+            whole.unbind_device_input()
+
+    def fill(chunk, r):
+        r0, r1 = bands[r]
+        chunk[:(r1 - r0) * W].copy_(whole_img[r0:r1].reshape(-1))
+
+    recv, secs = mg.scatter_images(per, fill, dist=dist, device=dev if backend == "nccl" else "cpu", dtype=dt)
+    recv = recv.to(dev)
+    r0, r1 = bands[rank]
+    ctx.build()
+    ctx.sync()
+    local = ctx.checksum(0)
+    ctx.bind_device_input(recv.data_ptr(), W, max(1, r1 - r0) * W, keepalive=recv)
+    ctx.build()
+    ctx.sync()
+    got = ctx.checksum(0)
+    ctx.unbind_device_input()
+    secs, bad = mg.max_over_ranks([secs, float(local != got)], dist=dist,
+                                  device="cuda" if backend == "nccl" else "cpu")
+    nbytes = sum(r1 - r0 for r0, r1 in bands[1:]) * W * (1 if in_fmt == "u8" else 4)
+    return {"mode": f"collective scatter of rank 0's image in row bands ({'RCCL over xGMI' if backend == 'nccl' else backend + ' via host'}), "
+                    "outside the timed region", "bytes_to_other_ranks": nbytes, "ms": round(secs * 1e3, 3),
+            "GBps": round(nbytes / secs / 1e9, 1) if secs > 0 else None, "bit_exact": bad == 0.0}
+
+
+def gather_bands(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
+    """The row-band config's output gather (optional; the MPI variant's collector,
+    GaussDePyramid-MPI.h:285-298): every rank packs its band pyramid, one collective gather brings
+    the bands to rank 0 (timed between barriers), and rank 0 lays them into a whole-image context
+    and checks gdp_checksum of the assembled pyramid against the reference's output for the
+    image.  Outside the timed region."""
+    import torch
+
+    import __graft_entry__ as entry
+
+    H, W, S, O = cfg["H"], cfg["W"], 2, cfg["O"]
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    def aligned(nbytes):  # 256-B aligned float32 view for gdp_set_output_device
+        raw = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=dev)
+        shift = (-raw.data_ptr() % 256) // 4
+        return raw, raw[shift:shift + nbytes // 4]
+
+    raw, view = aligned(ctx.pyramid_bytes())
+    ctx.bind_device_output(view.data_ptr(), ctx.pyramid_bytes(), keepalive=raw)
+    ctx.build()
+    ctx.sync()
+    parts = []
+    for o in range(O):
+        rows, cols, _ = ctx.level_dims(o)
+        for s in range(S + 3):
+            off = ctx.level_offset(0, o, s)
+            parts.append(view[off:off + rows * cols])
+    packed = torch.cat(parts) if parts else view[:0].clone()
+    ctx.unbind_device_output()
+    del raw, view, parts
+    sizes = [mg.packed_band_floats(H, W, S, O, *mg.plan_band(H, world, r, O)) for r in range(world)]
+    bands, secs = mg.gather_packed_bands(packed if backend == "nccl" else packed.cpu(), sizes, dist=dist)
+    del packed
+    secs = mg.max_over_ranks([secs], dist=dist, device="cuda" if backend == "nccl" else "cpu")[0]
+    if rank != 0:
+        return None
+    full = mg.assemble_bands(H, W, S, O, world, [b.to(dev) for b in bands])
+    del bands
+    pkg = entry.load_package()
+    with pkg.PyramidContext(H, W, S=S, octaves=O, batch=1, device=ctx.device, input_format=in_fmt) as whole:
+        wraw, wview = aligned(whole.pyramid_bytes())
+        whole.bind_device_output(wview.data_ptr(), whole.pyramid_bytes(), keepalive=wraw)
+        wview.zero_()
+        at = 0
+        for o in range(O):
+            rows, cols, _ = whole.level_dims(o)
+            for s in range(S + 3):
+                off = whole.level_offset(0, o, s)
+                wview[off:off + rows * cols] = full[at:at + rows * cols]
+                at += rows * cols
+        torch.cuda.synchronize()
+        got = whole.checksum(0)
+        whole.unbind_device_output()
+    want = _fixture_checksums(cfg).get(0)
+    nbytes = 4 * sum(sizes[1:])
+    return {"mode": f"collective gather of every row band's pyramid to rank 0 ({'RCCL over xGMI' if backend == 'nccl' else backend + ' via host'}), "
+                    "outside the timed region", "bytes_to_rank0": nbytes, "ms": round(secs * 1e3, 3),
+            "GBps": round(nbytes / secs / 1e9, 1) if secs > 0 else None,
+            "assembled_checksum": f"{got:016x}",
+            "status": ("unchecked (no reference fixture)" if want is None else
+                       "bit-exact vs the reference's output for the whole image" if got == want[0] else "MISMATCH")}
 
 
 def _fixture_checksums(cfg):
@@ -423,8 +534,12 @@ def main():
                     help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
                          "after their input rows; default 4)")
     ap.add_argument("--scatter", action="store_true",
-                    help="N > 1, image configs: also measure the image-batch split (rank 0's batch scattered over "
-                         "RCCL, SURVEY.md §8e), outside the timed region, and check the ranks build the same bits from it")
+                    help="N > 1: also measure the input split (rank 0's image batch, or for the row-band config its "
+                         "image's rows, scattered over RCCL, SURVEY.md §8e), outside the timed region, and check the "
+                         "ranks build the same bits from it")
+    ap.add_argument("--gather", action="store_true",
+                    help="N > 1, row-band config: also measure the collector's gather of every band's pyramid to "
+                         "rank 0 (outside the timed region) and check the assembled pyramid against the reference")
     ap.add_argument("--rotate", type=int, default=None,
                     help="independent input+pyramid buffer sets the steps cycle through (default: enough to "
                          "exceed %d MiB, so no step finds its lines in the 256 MB Infinity Cache)" % (ROTATE_BYTES >> 20))
@@ -518,7 +633,7 @@ def main():
     torch.cuda.set_stream(stream)
 
     distribution = None
-    if args.scatter and world > 1 and not cfg["band"]:
+    if args.scatter and world > 1 and not halo_exchange:
         distribution = scatter_split(ctx, cfg, world, rank, dist, mg, backend, args.input)
     for c in ctxs:
         c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order)
@@ -592,6 +707,9 @@ def main():
         parity["rotated_sets_agree"] = len(sums) == 1
         if len(sums) != 1:
             parity["status"] = "MISMATCH (rotated sets differ)"
+    collect = None
+    if args.gather and world > 1 and cfg["band"] and args.op == "build":
+        collect = gather_bands(ctx, cfg, world, rank, dist, mg, backend, args.input)
 
     # roofline of the (only) kernel of a step, per launch on THIS rank's share
     rows_local = ctx.row_end - ctx.row_begin
@@ -664,6 +782,8 @@ def main():
         if args.op == "conv" else {"status": "not checked for in-place re-entry ops"})
     if distribution is not None:
         result["distribution"] = distribution
+    if collect is not None:
+        result["collect"] = collect
     if args.op != "build":
         result["metric"] = METRIC + (" [op=conv: true-Gaussian extension, not the reference's algorithm]"
                                      if args.op == "conv" else f" [op={args.op}: in-place pass]")

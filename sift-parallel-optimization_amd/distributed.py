@@ -183,6 +183,39 @@ def scatter_images(per_rank, fill, dist=None, device="cpu", dtype=None):
     return recv, time.perf_counter() - t0
 
 
+def gather_packed_bands(band, sizes, dist=None, dst=0):
+    """The collector's exchange as ONE collective (the reference sends every level row by row,
+    MPI_Send / MPI_Recv at GaussDePyramid-MPI.h:285,298): each rank's packed band pyramid `band`
+    (sizes[r] float32 elements on rank r) is padded to the largest band and gathered to rank `dst`
+    (RCCL over xGMI for GPU tensors, gloo for CPU tensors).  Returns (the per-rank bands trimmed to
+    their sizes on `dst`, None elsewhere; seconds of the gather between two barriers)."""
+    import time
+
+    import torch
+
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    if world == 1:
+        return [band[:sizes[0]]], 0.0
+    if band.numel() != sizes[rank]:
+        raise ValueError(f"rank {rank}: band of {band.numel()} floats, plan says {sizes[rank]}")
+    buf = torch.zeros(max(sizes), dtype=torch.float32, device=band.device)
+    buf[:band.numel()] = band
+    gathered = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    sync = torch.cuda.synchronize if buf.is_cuda else (lambda: None)
+    sync()
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    dist.gather(buf, gathered, dst=dst)
+    sync()
+    secs = time.perf_counter() - t0
+    dist.barrier()
+    if rank != dst:
+        return None, secs
+    return [g[:sizes[r]] for r, g in enumerate(gathered)], secs
+
+
 def assemble_bands(H, W, S, octaves, world, packed_bands, like=None):
     """Collector-side assembly: the packed band pyramids of ranks 0..world-1 (torch tensors,
     any device) -> the packed pyramid of the whole image, in the oracle's [o][s][rows][cols]
@@ -233,15 +266,11 @@ def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None
     band = compute(np.ascontiguousarray(img[r0:r1]), r0, r1)
     if world == 1:
         return assemble_bands(n, n, S, O, 1, [band])
-    # equal-size buffers for the gather: pad every band to the largest one
     sizes = [packed_band_floats(n, n, S, O, *plan_band(n, world, r, O)) for r in range(world)]
-    buf = torch.zeros(max(sizes), dtype=torch.float32, device=band.device)
-    buf[:band.numel()] = band
-    gathered = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, gathered, dst=0)
+    bands, _ = gather_packed_bands(band, sizes, dist=dist, dst=0)
     if rank != 0:
         return None
-    return assemble_bands(n, n, S, O, world, [g[:sizes[r]] for r, g in enumerate(gathered)])
+    return assemble_bands(n, n, S, O, world, bands)
 
 
 def _gpu_band_compute(H, W, S, O, device, centre="serial"):

@@ -1039,3 +1039,23 @@ def test_bench_selflaunched_ranks_certify_their_work():
         else:
             assert line["parity"]["status"] == "bands == whole image (bit-exact)", line["parity"]
             assert "halo exchange" in line["roofline"]["step_includes"]
+
+
+@pytest.mark.gpu
+def test_bench_band_scatter_and_gather_collector():
+    """bench.py --config c5 --gpus 2 --scatter --gather (ranks over gloo on this one GPU): rank 0's
+    image scattered in row bands builds the same bits as the locally generated bands, and the
+    collector's gather of both band pyramids, laid into a whole-image context on rank 0, has the
+    checksum of the reference's output for the 16384^2 image (SURVEY.md §8e's optional paths)."""
+    import json
+
+    env = dict(os.environ, GDP_BENCH_BACKEND="gloo")
+    r = subprocess.run(["python3", os.path.join(REPO, "bench.py"), "--gpus", "2", "--config", "c5", "--steps", "2",
+                        "--warmup", "1", "--no-cpu", "--no-autotune", "--scatter", "--gather"],
+                       env=env, timeout=280, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["parity"]["status"] == "bit-exact", line["parity"]
+    assert line["distribution"]["bit_exact"] is True, line["distribution"]
+    assert line["collect"]["status"] == "bit-exact vs the reference's output for the whole image", line["collect"]
+    assert line["collect"]["bytes_to_rank0"] > 0
