@@ -164,7 +164,7 @@ def latest_conv_pmc(config_key, tun):
     return best
 
 
-def latest_pmc(config_key, variant, tile_order):
+def latest_pmc(config_key, variant, tile_order, op="build"):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
     whose recorded build variant and tile order equal the run's; None when no profile of that
@@ -179,7 +179,7 @@ def latest_pmc(config_key, variant, tile_order):
                         rec = json.load(fh)
                 except (OSError, ValueError):
                     continue
-                if rec.get("config") == config_key and rec.get("op", "build") == "build" and \
+                if rec.get("config") == config_key and rec.get("op", "build") == op and \
                         rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
                         rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32":
                     best = dict(rec, file=f)
@@ -229,12 +229,12 @@ def launch_ranks(n, argv, script=None):
     return rc
 
 
-def autotune_rotating(ctxs, stream, iters, rounds=5):
+def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
     """gdp_autotune's search (every build variant x tile order 0/1) over the ROTATED step sequence
     the benchmark times (one set when it alone exceeds the MALL), so the pick is made on cold
     buffers; candidates are interleaved round-robin over `rounds` rounds and ranked by their
     median (drift hits all alike, unlike gdp_autotune's one-candidate-at-a-time timing).  All
-    candidates give identical bits."""
+    candidates give identical bits.  op "subset" times the subset build (gdp_build_subset)."""
     import torch
 
     import __graft_entry__ as entry
@@ -252,12 +252,13 @@ def autotune_rotating(ctxs, stream, iters, rounds=5):
         for v, order in cands:
             for c in ctxs:
                 c.set_tuning(variant=v, tile_order=order)
-            for c in ctxs:
-                c.build(stream)
+            run = [c.build_subset if op == "subset" else c.build for c in ctxs]
+            for r in run:
+                r(stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for i in range(iters * len(ctxs)):
-                ctxs[i % len(ctxs)].build(stream)
+                run[i % len(ctxs)](stream)
             e1.record(stream)
             e1.synchronize()
             times[(v, order)].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
@@ -419,7 +420,7 @@ def gather_bands(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
                        "bit-exact vs the reference's output for the whole image" if got == want[0] else "MISMATCH")}
 
 
-def _fixture_checksums(cfg):
+def _fixture_checksums(cfg, subset=False):
     """global image index -> the gdp_checksum of the reference's output for that synthetic image
     (tests/golden/checksums.json; square images, generated by the reference binary), or of the
     oracle's closed form for non-square images (checksums_oracle.json: the reference only builds
@@ -427,6 +428,12 @@ def _fixture_checksums(cfg):
     H, W, O = cfg["H"], cfg["W"], cfg["O"]
     prefix = f"synth:{SEED:#x}:".lower()
     out = {}
+    if subset:  # GenerateDoG_nomp_dynamic's output (tests/golden/checksums_a512omp.json, the reference header)
+        with open(os.path.join(REPO, "tests", "golden", "checksums_a512omp.json")) as f:
+            for r in json.load(f):
+                if r["n"] == H == W and r["S"] == 2 and r["input"].lower().startswith(prefix) and f"octaves_{O}" in r:
+                    out[int(r["input"].split(":")[2])] = (int(r[f"octaves_{O}"], 16), "reference")
+        return out
     if H == W:
         with open(os.path.join(REPO, "tests", "golden", "checksums.json")) as f:
             for r in json.load(f):
@@ -440,13 +447,13 @@ def _fixture_checksums(cfg):
     return out
 
 
-def verify(ctx, cfg, key, world, rank, dist, mg, first_image):
+def verify(ctx, cfg, key, world, rank, dist, mg, first_image, subset=False):
     """After the timed region: gdp_checksum of what the benchmark built vs the checksum of the
     reference's own output for the same input.  Image configs: EVERY rank checksums the first and
     last image of its shard and rank 0 checks each against the fixtures (tests/golden/), so an
     N-rank line certifies every rank's images; the row-band config sums every rank's band
     checksum into the image's."""
-    fixtures = _fixture_checksums(cfg)
+    fixtures = _fixture_checksums(cfg, subset)
     if cfg["band"]:
         sums = mg.gather_checksums([ctx.checksum(0)], dist=dist)
         if rank != 0:
@@ -478,7 +485,8 @@ def verify(ctx, cfg, key, world, rank, dist, mg, first_image):
             "checked": f"first and last image of each of {world} rank(s): global images {sorted(checked + bad)}",
             "bit_exact_images": len(checked), "mismatched_images": bad, "images_without_fixture": unchecked,
             "ranks_certified": sorted({i // B for i in checked} - {i // B for i in bad}),
-            "against": ("reference output (tests/golden/checksums.json)" if against == {"reference"} else
+            "against": (("reference output (tests/golden/checksums_a512omp.json: GenerateDoG_nomp_dynamic)" if subset
+                         else "reference output (tests/golden/checksums.json)") if against == {"reference"} else
                         "oracle closed form (non-square input: no reference output exists)")}
 
 
@@ -522,7 +530,7 @@ def main():
                          "variant on this device before the warm-up; all variants give identical bits)")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
                     help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
-    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv"],
+    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv", "subset"],
                     help="build: fused GaussPyInit+GenerateDoG (headline); regen: in-place GenerateDoG "
                          "re-entry; gauss: in-place row+column window pass of every octave; conv: the "
                          "true-Gaussian-convolution extension (not the reference's algorithm)")
@@ -637,15 +645,19 @@ def main():
         distribution = scatter_split(ctx, cfg, world, rank, dist, mg, backend, args.input)
     for c in ctxs:
         c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order)
+        if args.op == "subset":  # that header's integer-length window centre (the same taps at these sizes)
+            c.set_window_centre("intlen")
     autotuned = None
     if args.variant is not None:
         for c in ctxs:
             c.set_tuning(variant=args.variant, tile_order=args.tile_order)
-    elif args.op == "build" and not args.no_autotune:
+    elif args.op in ("build", "subset") and not args.no_autotune:
         # candidates interleaved round-robin (drift hits all alike), over the rotated sets
-        autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10)
+        autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10, op=args.op)
     if args.op == "build":
         steps_fn = [c.build for c in ctxs]
+    elif args.op == "subset":  # GaussPyramid_a512omp::GenerateDoG_nomp_dynamic, the CPU baseline's semantics
+        steps_fn = [c.build_subset for c in ctxs]
     elif args.op == "conv" and halo_exchange:
         def conv_step(i, st):
             inp, top, bot, host = halos[i]
@@ -698,7 +710,8 @@ def main():
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
     wall, kernel_ms = mg.max_over_ranks([wall, kernel_ms], dist=dist, device=red_dev)
-    parity = verify(ctx, cfg, args.config, world, rank, dist, mg, first_image) if args.op == "build" else None
+    parity = (verify(ctx, cfg, args.config, world, rank, dist, mg, first_image, subset=args.op == "subset")
+              if args.op in ("build", "subset") else None)
     if halo_exchange:
         parity = verify_conv_bands(ctx, cfg, world, rank, dist, mg, args.input)
     if parity is not None and rotate > 1:
@@ -714,7 +727,7 @@ def main():
     # roofline of the (only) kernel of a step, per launch on THIS rank's share
     rows_local = ctx.row_end - ctx.row_begin
     pyr_px = sum(ctx.level_dims(o)[0] * ctx.level_dims(o)[1] for o in range(O)) * (1 if cfg["band"] else B)
-    if args.op not in ("build", "conv"):  # in-place passes read and write every level once: 8*(S+3)*P bytes
+    if args.op not in ("build", "conv", "subset"):  # in-place passes read and write every level once: 8*(S+3)*P bytes
         bytes_launch = 8 * (S + 3) * pyr_px
     elif cfg["band"]:
         bytes_launch = in_bytes * rows_local * W + 4 * (S + 3) * pyr_px
@@ -723,8 +736,8 @@ def main():
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
     tun = ctx.tuning()
     # PMC records are of the whole workload on one GPU: a row band (config 5 at N > 1) is another launch
-    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"])
-           if args.op == "build" and args.input == "i32" and not (cfg["band"] and world > 1) else None)
+    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op)
+           if args.op in ("build", "subset") and args.input == "i32" and not (cfg["band"] and world > 1) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
 
@@ -762,6 +775,9 @@ def main():
             "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d%s"
                        % (ctx.tuning()["variant"], ctx.tuning()["tile_order"], " (autotuned)" if autotuned else "")
                        if args.op == "build" else
+                       "k_build<SUB> (fused decimate+window+DoG, GenerateDoG_nomp_dynamic's subset of levels), "
+                       "variant %d, tile order %d" % (ctx.tuning()["variant"], ctx.tuning()["tile_order"])
+                       if args.op == "subset" else
                        {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
                         "gauss": "k_window (in-place row+column window, all octaves)",
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
@@ -777,7 +793,7 @@ def main():
             "algorithmic_bytes_per_launch": bytes_launch,
         },
     }
-    result["parity"] = parity if (args.op == "build" or halo_exchange) else (
+    result["parity"] = parity if (args.op in ("build", "subset") or halo_exchange) else (
         {"status": "extension: no reference output (tests/ check it against a float64 convolution)"}
         if args.op == "conv" else {"status": "not checked for in-place re-entry ops"})
     if distribution is not None:
@@ -786,7 +802,10 @@ def main():
         result["collect"] = collect
     if args.op != "build":
         result["metric"] = METRIC + (" [op=conv: true-Gaussian extension, not the reference's algorithm]"
-                                     if args.op == "conv" else f" [op={args.op}: in-place pass]")
+                                     if args.op == "conv" else
+                                     " [op=subset: GaussPyramid_a512omp::GenerateDoG_nomp_dynamic's output, the "
+                                     "CPU baseline's own semantics]" if args.op == "subset" else
+                                     f" [op={args.op}: in-place pass]")
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
     elif rank == 0:

@@ -134,6 +134,18 @@ int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);
  * (GuassDePyramid.h:136-149).  After gdp_init this equals gdp_build; called again it re-filters,
  * like the reference's repeated-call timing loop (main.cpp:66-73). */
 int gdp_generate_dog(gdp_ctx* ctx, void* stream);
+/* GaussPyramid_a512omp::GenerateDoG_nomp_dynamic (GaussDePyramid-AVX512xOpenMP.h:240-364), the
+ * reference's AVX-512 x OpenMP path, whose output is a SUBSET of GenerateDoG's: only scales
+ * 0..S-1 are windowed (:242-318) and level i -= level i+1 only for i < S-1 (:337-357), so the
+ * pyramid holds {DoG_0..DoG_{S-2}, G_{S-1}, x, x, x} with x the GaussPyInit value.  The header
+ * computes its windows with the integer-length centre float(len_o - 1) / 2 (:251, :279): use
+ * GDP_CENTRE_INTLEN (gdp_set_window_centre) to reproduce it (identical to the serial centre when
+ * the side is a multiple of 2^(octaves-1), the only sizes its 16-float vector loops handle).
+ *   gdp_build_subset:        fused GaussPyInit + GenerateDoG_nomp_dynamic from the input
+ *   gdp_generate_dog_subset: GenerateDoG_nomp_dynamic in place on the CURRENT contents (repeated
+ *                            calls re-filter, like the reference's timing loop) */
+int gdp_build_subset(gdp_ctx* ctx, void* stream);
+int gdp_generate_dog_subset(gdp_ctx* ctx, void* stream);
 
 /* ---- extension: true Gaussian convolution pyramid --------------------------
  * NOT the reference's algorithm (which multiplies by a window, :119-131) and carries no parity

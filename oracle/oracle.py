@@ -145,6 +145,18 @@ def subset_a512omp(pyr, H, W, S, O):
     return pyr
 
 
+def generate_dog_a512omp(pyr, H, W, S, O):
+    """GaussPyramid_a512omp::GenerateDoG (GaussDePyramid-AVX512xOpenMP.h:183-213): that class's
+    GaussFilter is empty (:128-181, its body commented out), so per octave only the DoG pass
+    level j -= level j+1 for j = 0..S+1 runs (:187-193) — and a second time when the octave's
+    integer side length is <= 2 (:194-201)."""
+    for o in range(O):
+        dog_octave(pyr, H, W, S, o)
+        if min(H, W) >> o <= 2:
+            dog_octave(pyr, H, W, S, o)
+    return pyr
+
+
 def fnv(a):
     a = np.ascontiguousarray(a, dtype=np.float32)
     return lib().gdo_fnv(_ptr(a), a.size)

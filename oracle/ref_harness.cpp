@@ -10,8 +10,13 @@
 //   ref_harness dump   <n> <S> <input> <out.f32>           all levels, packed [o][s][r][c] float32
 //   ref_harness taps   <n> <S> <out.f32>                   reference `filter` taps for every (o, s)
 //   ref_harness regen  <n> <S> <input> <calls> <out.f32>   GenerateDoG() called <calls> times
+//   ref_harness regen-hash <n> <S> <input> <calls>         per-level FNV hashes of the same
 //   ref_harness dump-a512omp <n> <S> <input> <out.f32>     GenerateDoG_nomp_dynamic() output
 //   ref_harness dump-a512xp  <n> <S> <input> <out.f32>     GaussPyramid_a512xp::GenerateDoG() output
+//   ref_harness hash-a512omp <n> <S> <input> <calls> <method> [threads]  per-level FNV hashes after
+//               <calls> calls of GaussPyramid_a512omp::<method>, method "nomp_dynamic" or
+//               "GenerateDoG" (or of GaussPyramid_a512xp::GenerateDoG: "xp.GenerateDoG"), with `counnt` = threads (default 1: its DoG loop, an `omp for` over
+//               i < S-1 doing level i -= level i+1 in place, races between threads once S >= 3)
 //   ref_harness time-serial  <n> <S> <input> <reps>
 //   ref_harness time-a512omp <n> <S> <input> <reps> <threads>
 //   ref_harness time-a512xp  <n> <S> <input> <reps>
@@ -115,6 +120,11 @@ int main(int argc, char** argv) {
             hash(g.GaussPy, n, S);
         else
             dump(g.GaussPy, n, S, argv[5]);
+    } else if (mode == "regen-hash") {
+        GaussPyramid g(img, n, S);
+        const int calls = std::atoi(argv[5]);
+        for (int c = 0; c < calls; ++c) g.GenerateDoG();
+        hash(g.GaussPy, n, S);
     } else if (mode == "regen") {
         GaussPyramid g(img, n, S);
         const int calls = std::atoi(argv[5]);
@@ -125,6 +135,27 @@ int main(int argc, char** argv) {
         GaussPyramid_a512omp g(img, n, S);
         g.GenerateDoG_nomp_dynamic();
         dump(g.GaussPy, n, S, argv[5]);
+    } else if (mode == "hash-a512omp") {
+        if (argc < 7) return 2;
+        counnt = argc > 7 ? std::atoi(argv[7]) : 1;  // GaussDePyramid-AVX512xOpenMP.h:18
+        const int calls = std::atoi(argv[5]);
+        const std::string method = argv[6];
+        if (method == "xp.GenerateDoG") {
+            GaussPyramid_a512xp g(img, n, S);
+            for (int c = 0; c < calls; ++c) g.GenerateDoG();
+            hash(g.GaussPy, n, S);
+            return 0;
+        }
+        GaussPyramid_a512omp g(img, n, S);
+        for (int c = 0; c < calls; ++c) {
+            if (method == "nomp_dynamic")
+                g.GenerateDoG_nomp_dynamic();
+            else if (method == "GenerateDoG")
+                g.GenerateDoG();
+            else
+                return 2;
+        }
+        hash(g.GaussPy, n, S);
     } else if (mode == "dump-a512xp") {
         GaussPyramid_a512xp g(img, n, S);
         g.GenerateDoG();

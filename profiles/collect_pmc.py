@@ -62,7 +62,7 @@ def main():
     fetch = counter_values(os.path.join(args.fetch, "run_counter_collection.csv"), "FETCH_SIZE", name)
     write = counter_values(os.path.join(args.write, "run_counter_collection.csv"), "WRITE_SIZE", name)
     cfg = bench.CONFIGS[args.config]
-    if args.op in ("build", "conv"):
+    if args.op in ("build", "conv", "subset"):
         alg = bench.algorithmic_bytes(cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"])
     else:  # in-place passes read and write every level: 8*(S+3)*P
         alg = 8 * 5 * cfg["batch"] * bench.pyramid_pixels(cfg["H"], cfg["W"], cfg["O"])

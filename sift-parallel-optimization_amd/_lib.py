@@ -71,6 +71,8 @@ SIGNATURES = {
     "gdp_gauss_range": (_c_int, [_p, _c_int, _c_int, _p]),
     "gdp_dog_octave": (_c_int, [_p, _c_int, _p]),
     "gdp_generate_dog": (_c_int, [_p, _p]),
+    "gdp_build_subset": (_c_int, [_p, _p]),
+    "gdp_generate_dog_subset": (_c_int, [_p, _p]),
     "gdp_device_level": (_p, [_p, _c_int, _c_int, _c_int]),
     "gdp_download_level": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_download_level_rows": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),

@@ -183,7 +183,7 @@ int upload_geom(gdp_ctx* c) {
     return GDP_OK;
 }
 
-int launch_build(gdp_ctx* c, hipStream_t st) {
+int launch_build(gdp_ctx* c, hipStream_t st, bool subset = false) {
     const Geom& g = c->geom;
     const long long units = (long long)g.tiles_total + g.tail_units;
     if (units == 0) return GDP_OK;
@@ -191,8 +191,9 @@ int launch_build(gdp_ctx* c, hipStream_t st) {
     const long long cap = c->grid_override > 0 ? c->grid_override : (c->persistent ? c->blocks_max : units);
     const int grid = (int)std::min<long long>(units, cap);
     const BuildVariant& v = kVariants[c->variant];
-    hipLaunchKernelGGL(v.k[g.L == 5][c->nontemporal ? 1 : 0], dim3(grid), dim3(v.block), (unsigned)c->build_lds, st,
-                       c->d_geom, c->d_in, c->d_out, c->d_taps);
+    auto kern = (subset ? v.ksub : v.k)[g.L == 5][c->nontemporal ? 1 : 0];
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(v.block), (unsigned)c->build_lds, st, c->d_geom, c->d_in, c->d_out,
+                       c->d_taps);
     GDP_HIP(c, hipGetLastError());
     return GDP_OK;
 }
@@ -215,8 +216,10 @@ int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     const long long grid = per * g.batch * SUB;
     if (grid <= 0) return GDP_OK;
     if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "in-place pass too large for one launch");
-    auto kern = g.L == 5 ? (c->nontemporal ? k_levels<5, MODE, true, SUB> : k_levels<5, MODE, false, SUB>)
-                         : (c->nontemporal ? k_levels<0, MODE, true, SUB> : k_levels<0, MODE, false, SUB>);
+    auto kern = c->nontemporal ? k_levels<0, MODE, true, SUB> : k_levels<0, MODE, false, SUB>;
+    if constexpr (MODE != 9) {
+        if (g.L == 5) kern = c->nontemporal ? k_levels<5, MODE, true, SUB> : k_levels<5, MODE, false, SUB>;
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kLevBlock / SUB), 0, st, c->d_geom, c->d_in, c->d_out, c->d_taps,
                        ob, oe);
     GDP_HIP(c, hipGetLastError());
@@ -969,6 +972,18 @@ int gdp_generate_dog(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<3>(c, 0, c->geom.O, c->pick(stream));
+} GDP_ABI_CATCH(c)
+
+int gdp_build_subset(gdp_ctx* c, void* stream) try {
+    if (!c) return GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_build(c, c->pick(stream), true);
+} GDP_ABI_CATCH(c)
+
+int gdp_generate_dog_subset(gdp_ctx* c, void* stream) try {
+    if (!c) return GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace_sub<9, 1>(c, 0, c->geom.O, c->pick(stream));
 } GDP_ABI_CATCH(c)
 
 const float* gdp_device_level(const gdp_ctx* c, int b, int o, int s) {

@@ -220,6 +220,15 @@ class PyramidContext:
     def generate_dog(self, stream=None):
         check(lib().gdp_generate_dog(self._ctx, _stream_handle(stream)), self._ctx)
 
+    def build_subset(self, stream=None):
+        """Fused GaussPyInit + GaussPyramid_a512omp::GenerateDoG_nomp_dynamic (the AVX-512 x OpenMP
+        header's subset: scales 0..S-1 windowed, DoG for s < S-1; see gdp.h)."""
+        check(lib().gdp_build_subset(self._ctx, _stream_handle(stream)), self._ctx)
+
+    def generate_dog_subset(self, stream=None):
+        """GenerateDoG_nomp_dynamic in place on the current contents."""
+        check(lib().gdp_generate_dog_subset(self._ctx, _stream_handle(stream)), self._ctx)
+
     def sync(self):
         check(lib().gdp_sync(self._ctx), self._ctx)
 

@@ -19,10 +19,14 @@ Outputs (all plain data, loadable without pickle):
                 variants — GaussPyramid_mpi::GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335) and
                 mpitest.cpp's GenerateDoG_mpi / GenerateDoG_mpi_omp (:35-189) — run under
                 conda MPICH's mpiexec with S+4 ranks (oracle/_ref/ref_mpi, ref_mpitest)
+  checksums_a512omp.json gdp_checksum values of GenerateDoG_nomp_dynamic's output for the bench inputs
+  a512_hashes.json per-level hashes after repeated calls of GaussPyramid_a512omp's
+                GenerateDoG_nomp_dynamic (the AVX-512 x OpenMP subset, :240-364) and GenerateDoG
+                (its DoG-only form, :183-213) — oracle/_ref/ref_avx512 hash-a512omp
   meta.json     generator provenance (glibc, g++, input definitions)
 
 Usage:  make -C oracle ref ref-mpi && python tests/golden/gen_golden.py [--only PART,...]
-        PART: hashes, dumps, taps, checksums, mpi (default: all)
+        PART: hashes, dumps, taps, checksums, mpi, a512 (default: all)
 """
 import json
 import os
@@ -77,6 +81,19 @@ MPI_CASES = [(v, n, S, inp) for v in ("GaussDePyramid-MPI.h:GenerateDoG_mpi", "m
                                        "mpitest.cpp:GenerateDoG_mpi_omp")
              for n, S, inp in [(512, 2, "lcg:12345"), (256, 2, "ones"), (256, 2, "lcg:12345"),
                                (100, 2, "lcg:12345"), (1000, 2, "lcg:12345"), (96, 1, "lcg:7")]]
+# GaussPyramid_a512omp / _a512xp methods, (method, n, S, input, calls): power-of-two n only (its 16-float
+# vector loops run past the row end otherwise); n <= 8 octaves take its scalar branch
+A512_CASES = [("nomp_dynamic", n, S, inp, calls) for n, S, inp, calls in [
+    (64, 2, "lcg:12345", 1), (256, 2, "lcg:12345", 2), (512, 2, "lcg:12345", 1), (512, 2, "ones", 3),
+    (1024, 3, "lcg:7", 1), (2048, 1, "lcg:5", 2), (16, 2, "lcg:3", 1), (8, 2, "lcg:3", 2), (256, 5, "lcg:9", 1),
+    (128, 0, "lcg:1", 1), (4096, 2, "synth:0x5EED:0", 1)]] + \
+    [("GenerateDoG", n, S, inp, calls) for n, S, inp, calls in [
+        (64, 2, "lcg:12345", 1), (64, 2, "lcg:12345", 2), (256, 3, "ones", 1), (512, 2, "lcg:12345", 1),
+        (16, 2, "lcg:3", 3)]] + \
+    [("xp.GenerateDoG", n, S, inp, calls) for n, S, inp, calls in [
+        (3, 2, "lcg:12345", 1), (5, 2, "lcg:12345", 1), (6, 1, "lcg:4", 2), (7, 3, "lcg:12345", 1),
+        (64, 2, "lcg:12345", 2), (512, 2, "lcg:12345", 1)]]
+A512_CHECKSUM_CASES = [(4096, 2, "synth:0x5EED:0"), (4096, 2, "synth:0x5EED:1")]
 TAP_CASES = [(512, 2), (100, 2), (1000, 2), (513, 3), (4096, 2), (1080, 2), (1920, 2), (37, 1)]
 
 
@@ -175,13 +192,55 @@ def gen_mpi():
         json.dump(out, f, indent=1)
 
 
+def gen_a512():
+    if not os.path.exists(REF_AVX512):
+        sys.exit(f"missing {REF_AVX512}: run `make -C oracle ref` first")
+    out = []
+    for method, n, S, inp, calls in A512_CASES:
+        # counnt = 1: with more threads its DoG loop (an `omp for` over i < S-1, level i -= level
+        # i+1 in place, :324-357) is a data race once S >= 3 — the output is then timing-dependent
+        rec = json.loads(run(REF_AVX512, "hash-a512omp", str(n), str(S), inp, str(calls), method, "1"))
+        name = {"nomp_dynamic": "GaussPyramid_a512omp::GenerateDoG_nomp_dynamic",
+                "GenerateDoG": "GaussPyramid_a512omp::GenerateDoG",
+                "xp.GenerateDoG": "GaussPyramid_a512xp::GenerateDoG"}[method]
+        rec.update({"method": name, "input": inp, "calls": calls, "counnt": 1})
+        if method == "xp.GenerateDoG":  # recorded as a fact about the reference
+            ser = json.loads(run(REF_SERIAL, "regen-hash", str(n), str(S), inp, str(calls)))
+            rec["equals_serial"] = rec["octaves"] == ser["octaves"]
+        out.append(rec)
+        print("a512", method, n, S, inp, calls, flush=True)
+    with open(os.path.join(HERE, "a512_hashes.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    # gdp_checksum of GenerateDoG_nomp_dynamic's output for the bench inputs (bench.py --op subset)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # the checksum formula's numpy restatement (test infrastructure)
+
+    checks = []
+    for n, S, inp in A512_CHECKSUM_CASES:
+        pyr = dump(REF_AVX512, "dump-a512omp", n, S, inp)  # S = 2: one DoG iteration, no race
+        sl, _ = level_slices(n, S)
+        acc, rec = 0, {"n": n, "S": S, "input": inp, "method": "GaussPyramid_a512omp::GenerateDoG_nomp_dynamic"}
+        for o in range(octaves_of(n)):
+            m = n >> o
+            for s in range(S + 3):
+                off, _ = sl[(o, s)]
+                acc = (acc + oracle.level_checksum(pyr[off:off + m * m].reshape(m, m), o, s)) & 0xFFFFFFFFFFFFFFFF
+            rec[f"octaves_{o + 1}"] = f"{acc:016x}"
+        checks.append(rec)
+        print("a512 checksum", n, inp, flush=True)
+    with open(os.path.join(HERE, "checksums_a512omp.json"), "w") as f:
+        json.dump(checks, f, indent=1)
+
+
 def main():
-    parts = {"hashes", "dumps", "taps", "checksums", "mpi"}
+    parts = {"hashes", "dumps", "taps", "checksums", "mpi", "a512"}
     if "--only" in sys.argv:
         parts = set(sys.argv[sys.argv.index("--only") + 1].split(","))
     if "mpi" in parts:
         gen_mpi()
-    if not parts - {"mpi"}:
+    if "a512" in parts:
+        gen_a512()
+    if not parts - {"mpi", "a512"}:
         return
     for b in (REF_SERIAL, REF_AVX512):
         if not os.path.exists(b):

@@ -68,16 +68,20 @@ def test_create_without_gpu_fails_loudly(pkg):
         pkg.PyramidContext(64, 64, 2)
 
 
-def test_cpp_dropin_header_compiles_with_plain_gxx(tmp_path):
+@pytest.mark.parametrize("header,cls", [("GaussDePyramid-HIP.h", "GaussPyramid_hip"),
+                                        ("GaussDePyramid-HIP-AVX512.h", "GaussPyramid_a512omp_hip"),
+                                        ("GaussDePyramid-HIP-AVX512.h", "GaussPyramid_a512xp_hip")])
+def test_cpp_dropin_header_compiles_with_plain_gxx(tmp_path, header, cls):
     src = tmp_path / "t.cpp"
-    src.write_text('#include "GaussDePyramid-HIP.h"\nint main(){ GaussPyramid_hip g; (void)g; return 0; }\n')
-    subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Werror", "-I" + os.path.join(REPO, "include"),
+    src.write_text(f'#include "{header}"\nint main(){{ {cls} g; (void)g; return 0; }}\n')
+    subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I" + os.path.join(REPO, "include"),
                     str(src)], check=True)
 
 
 def test_example_driver_links():
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
     assert os.path.exists(os.path.join(REPO, "examples", "main_hip"))
+    assert os.path.exists(os.path.join(REPO, "examples", "a512_hip"))
 
 
 def test_product_never_reaches_the_oracle():

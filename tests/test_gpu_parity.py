@@ -1059,3 +1059,91 @@ def test_bench_band_scatter_and_gather_collector():
     assert line["distribution"]["bit_exact"] is True, line["distribution"]
     assert line["collect"]["status"] == "bit-exact vs the reference's output for the whole image", line["collect"]
     assert line["collect"]["bytes_to_rank0"] > 0
+
+
+# ------------------------------------------------------------ AVX-512 classes (a12 / a13 rows)
+def _a512_records(method):
+    import json
+
+    with open(os.path.join(REPO, "tests", "golden", "a512_hashes.json")) as f:
+        return [r for r in json.load(f) if r["method"] == method]
+
+
+def test_subset_build_matches_reference_a512omp(pkg, oracle):
+    """gdp_build_subset (fused) and gdp_generate_dog_subset (in place, repeated calls) == the
+    reference's GaussPyramid_a512omp::GenerateDoG_nomp_dynamic per level (a512_hashes.json:
+    n = 8 .. 4096 incl. the bench's own 4096^2 input, S = 0 .. 5, 1-3 calls), and the fused build
+    == GaussPyInit + the in-place pass on every bit."""
+    recs = _a512_records("GaussPyramid_a512omp::GenerateDoG_nomp_dynamic")
+    assert len(recs) >= 10
+    for rec in recs:
+        n, S, spec, calls = rec["n"], rec["S"], rec["input"], rec["calls"]
+        with pkg.PyramidContext(n, n, S=S) as ctx:
+            ctx.set_window_centre("intlen")
+            if spec.startswith("synth:"):
+                _, seed, idx = spec.split(":")
+                ctx.fill_synthetic(int(seed, 0), int(idx, 0))
+            else:
+                ctx.set_input(oracle.image_from_spec(n, spec))
+            ctx.build_subset()
+            for _ in range(calls - 1):
+                ctx.generate_dog_subset()
+            ctx.sync()
+            for o, row in enumerate(rec["octaves"]):
+                for s, h in enumerate(row):
+                    assert oracle.fnv(ctx.level(0, o, s)) == int(h, 16), (n, S, spec, calls, o, s)
+            if calls == 1:
+                fused = ctx.pyramid()
+                ctx.init()
+                ctx.generate_dog_subset()
+                _assert_same(ctx.pyramid(), fused, ("init + in-place subset", n, S))
+
+
+@pytest.mark.parametrize("H,W,S,B,fmt", [(100, 100, 2, 1, "i32"), (96, 160, 3, 3, "u8"), (513, 257, 1, 2, "i32"),
+                                         (64, 64, 0, 1, "i32")])
+def test_subset_build_matches_oracle_any_shape(pkg, oracle, H, W, S, B, fmt):
+    """Sizes the reference's vector loops cannot take (they overrun rows whose length is not a
+    multiple of 16): the subset semantics restated by the oracle (integer-length centres from W
+    for columns and H for rows), batches, uint8 input — no reference output exists (parity
+    against the oracle only)."""
+    rng = np.random.default_rng(H * 7 + W)
+    imgs = rng.integers(0, 256, size=(B, H, W)).astype(np.uint8 if fmt == "u8" else np.int32)
+    with pkg.PyramidContext(H, W, S=S, batch=B, input_format=fmt) as ctx:
+        ctx.set_window_centre("intlen")
+        for b in range(B):
+            ctx.set_input(imgs[b], b)
+        ctx.build_subset()
+        ctx.generate_dog_subset()
+        ctx.sync()
+        O = ctx.O
+        for b in range(B):
+            want = oracle.init_pyramid(imgs[b].astype(np.int32), S, O)
+            oracle.subset_a512omp(want, H, W, S, O)
+            oracle.subset_a512omp(want, H, W, S, O)
+            _assert_same(ctx.pyramid(b), want, ("subset x2", H, W, S, b))
+
+
+def test_cpp_a512_dropin_classes_match_reference(oracle, tmp_path):
+    """include/GaussDePyramid-HIP-AVX512.h through plain g++ (examples/a512_hip): the drop-in
+    GaussPyramid_a512omp_hip's GenerateDoG_nomp_dynamic and GenerateDoG, and
+    GaussPyramid_a512xp_hip's GenerateDoG, after 1-3 calls == the reference classes' output
+    (a512_hashes.json), incl. a512xp's integer-length centre on sides 3 / 5 / 6 / 7 where it
+    differs from the serial header."""
+    exe = os.path.join(REPO, "examples", "a512_hip")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples"), "a512_hip"], check=True)
+    out = tmp_path / "a.f32"
+    ran = 0
+    for method, tag in [("GaussPyramid_a512omp::GenerateDoG_nomp_dynamic", "nomp_dynamic"),
+                        ("GaussPyramid_a512omp::GenerateDoG", "GenerateDoG"),
+                        ("GaussPyramid_a512xp::GenerateDoG", "xp.GenerateDoG")]:
+        for rec in _a512_records(method):
+            n, S, spec, calls = rec["n"], rec["S"], rec["input"], rec["calls"]
+            if spec.startswith("synth:") or n > 1024:
+                continue  # the driver generates ones / lcg inputs; larger cases run above
+            subprocess.run([exe, tag, str(n), str(S), spec, str(calls), str(out)], check=True, timeout=120)
+            _assert_hashes(oracle, np.fromfile(out, dtype=np.float32), rec, tag)
+            ran += 1
+    assert ran >= 15
+    timing = subprocess.run([exe], check=True, timeout=120, capture_output=True, text=True).stdout.splitlines()
+    assert len(timing) == 2 and all(float(t.split()[0]) > 0 for t in timing), timing

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv"])
+    ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv", "subset"],
+                    help="default op; a variant may override it with op=... (e.g. 'v=15;v=15,op=subset')")
     ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
     ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
@@ -43,7 +44,7 @@ def main():
         c.fill_synthetic(bench.SEED, 0)
         c.sync()
     ctx = ctxs[0]
-    ref = None
+    refs = {}
     base_conv_order = ctx.tuning()["conv_order"]  # the library's geometry-dependent default
     variants = []
     for v in args.variants.split(";"):
@@ -53,6 +54,7 @@ def main():
                              "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1)),
                              "conv_kernel": int(kv.get("ck", 0)), "conv_rows": int(kv.get("cr", 16)),
                              "conv_order": int(kv.get("co", base_conv_order)), "conv_waves": int(kv.get("cw", 16)), "build_lds": int(kv.get("lds", 0))}))
+        variants[-1][1]["op"] = kv.get("op", args.op)
         if variants[-1][1]["variant"] is None:
             del variants[-1][1]["variant"]
         if "bpc" in kv:
@@ -61,34 +63,36 @@ def main():
 
     def apply(kw):  # fresh context state per variant: persistent only when bpc is given
         for c in ctxs:
-            c.set_tuning(**{k: v for k, v in kw.items() if k != "blocks_per_cu"})
+            c.set_tuning(**{k: v for k, v in kw.items() if k not in ("blocks_per_cu", "op")})
             c.set_tuning(blocks_per_cu=kw.get("blocks_per_cu", 0))
 
-    for name, kw in variants:  # warm-up + identical-output check for every variant
+    for name, kw in variants:  # warm-up + identical-output check for every variant (per op)
         apply(kw)
-        (ctx.build_gaussian if args.op == "conv" else ctx.build)()
+        {"conv": ctx.build_gaussian, "subset": ctx.build_subset}.get(kw["op"], ctx.build)()
         ctx.sync()
         lev = ctx.level(0, 0, 0)
-        if ref is None:
-            ref = lev
+        ref = refs.setdefault(kw["op"], lev)
         if args.no_check:
             pass
-        elif args.op == "conv":  # the two convolution kernels round differently (no parity contract)
+        elif kw["op"] == "conv":  # the two convolution kernels round differently (no parity contract)
             assert np.allclose(lev, ref, rtol=1e-5, atol=1e-3), name
         else:
             assert np.array_equal(lev.view(np.uint32), ref.view(np.uint32)), name
     import torch
 
     stream = torch.cuda.Stream()
-    steps = [{"build": c.build, "regen": c.generate_dog, "gauss": lambda st, c=c: c.gauss_range(0, O, st),
-              "conv": c.build_gaussian}[args.op] for c in ctxs]
-    if args.op in ("regen", "gauss"):
+    def steps_of(op):
+        return [{"build": c.build, "regen": c.generate_dog, "gauss": lambda st, c=c: c.gauss_range(0, O, st),
+                 "conv": c.build_gaussian, "subset": c.build_subset}[op] for c in ctxs]
+
+    if any(kw["op"] in ("regen", "gauss") for _, kw in variants):
         for c in ctxs:
             c.build(stream)
     for _ in range(args.rounds):
         for name, kw in variants:
             apply(kw)
-            if args.op == "build" and args.rotate == 1:
+            steps = steps_of(kw["op"])
+            if kw["op"] == "build" and args.rotate == 1:
                 times[name].append(ctx.time_builds(args.iters) / args.iters)
             else:
                 for st in steps:
@@ -100,7 +104,7 @@ def main():
                 e1.record(stream)
                 e1.synchronize()
                 times[name].append(e0.elapsed_time(e1) / args.iters)
-    if args.op in ("build", "conv"):
+    if args.op in ("build", "conv", "subset"):
         nbytes = bench.algorithmic_bytes(H, W, 2, O, B)
     else:
         nbytes = 8 * 5 * B * sum((H >> o) * (W >> o) for o in range(O))
