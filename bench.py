@@ -164,7 +164,7 @@ def latest_conv_pmc(config_key, tun):
     return best
 
 
-def latest_pmc(config_key, variant, tile_order, op="build"):
+def latest_pmc(config_key, variant, tile_order, op="build", levels=5):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
     whose recorded build variant and tile order equal the run's; None when no profile of that
@@ -179,9 +179,12 @@ def latest_pmc(config_key, variant, tile_order, op="build"):
                         rec = json.load(fh)
                 except (OSError, ValueError):
                     continue
+                # the template instance too: k_build<5, ...> (S + 3 = 5 levels unrolled) or k_build<0, ...>
+                lt = f"k_build<{5 if levels == 5 else 0},"
                 if rec.get("config") == config_key and rec.get("op", "build") == op and \
                         rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
-                        rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32":
+                        rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32" and \
+                        lt in rec.get("kernel", lt):
                     best = dict(rec, file=f)
     return best
 
@@ -736,7 +739,7 @@ def main():
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
     tun = ctx.tuning()
     # PMC records are of the whole workload on one GPU: a row band (config 5 at N > 1) is another launch
-    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op)
+    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3)
            if args.op in ("build", "subset") and args.input == "i32" and not (cfg["band"] and world > 1) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)

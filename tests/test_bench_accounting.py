@@ -122,3 +122,17 @@ def test_traffic_records_match_only_their_kernel_instance():
     conv = bench.latest_conv_pmc("c2", {"conv_kernel": 2, "conv_rows": 32, "conv_order": 4})
     assert conv is not None and conv["op"] == "conv"
     assert bench.latest_conv_pmc("c2", {"conv_kernel": 0, "conv_rows": 16, "conv_order": 0}) is None
+
+
+def test_subset_traffic_records_name_their_template_instance():
+    """bench.py --op subset attaches PMC traffic only from a record of the subset build's own
+    instance (op "subset", k_build<5, ..., true> for S = 2): never the full build's record of the
+    same variant, nor another template instance's."""
+    import bench
+
+    rec = bench.latest_pmc("c2", 15, 0, "subset", 5)
+    assert rec is not None and rec["op"] == "subset" and rec["kernel"].startswith("void (anonymous namespace)::k_build<5,")
+    assert "true>" in rec["kernel"]  # the SUB template flag
+    full = bench.latest_pmc("c2", 15, 0, "build", 5)
+    assert full is not None and full["file"] != rec["file"]
+    assert bench.latest_pmc("c2", 15, 0, "subset", 4) is None  # no k_build<0, ...> subset record

@@ -37,6 +37,8 @@ def run(args):
     ctxs = [pkg.PyramidContext(H, W, S=2, octaves=O, batch=B) for _ in range(rotate)]
     for c in ctxs:
         c.fill_synthetic(bench.SEED, 0)
+        if args.op == "subset":  # bench.py --op subset's contexts
+            c.set_window_centre("intlen")
         c.sync()
     order = []
     for v in range(64):
@@ -51,7 +53,7 @@ def run(args):
             c.set_tuning(variant=v, tile_order=t)
         n = 0
         for i in range(args.warm + args.reps):  # consecutive launches cycle through the cold sets
-            ctxs[i % rotate].build()
+            (ctxs[i % rotate].build_subset if args.op == "subset" else ctxs[i % rotate].build)()
             n += 1
         for c in ctxs:
             c.sync()
@@ -59,7 +61,7 @@ def run(args):
     for c in ctxs:
         c.close()
     with open(args.manifest, "w") as f:
-        json.dump({"config": args.config, "rotate": rotate, "instances": manifest}, f)
+        json.dump({"config": args.config, "op": args.op, "rotate": rotate, "instances": manifest}, f)
 
 
 def per_dispatch(d, counter):
@@ -90,7 +92,7 @@ def summarise(args):
         read_b = 2 * statistics.median(v for _, v, _ in fs) * 1024
         write_b = statistics.median(v for _, v, _ in ws) * 1024
         rec = {"config": man["config"], "round": args.round, "kernel": fs[0][2], "variant": m["variant"],
-               "tile_order": m["tile_order"], "input_format": "i32", "op": "build",
+               "tile_order": m["tile_order"], "input_format": "i32", "op": man.get("op", "build"),
                "source": "tools/pmc_variants.py: every instance in one process, its own FETCH_SIZE and WRITE_SIZE "
                          "rocprofv3 --pmc passes, launches cycling over %d cold buffer sets as in bench.py" % man["rotate"],
                "dispatches_counted": [len(fs), len(ws)],
@@ -99,7 +101,8 @@ def summarise(args):
                "kernel_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
                "traffic_over_algorithmic": (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads); write = WRITE_SIZE KiB"}
-        out = os.path.join(REPO, "profiles", f"pmc_{man['config']}_v{m['variant']}o{m['tile_order']}_{args.round}.json")
+        tag = man["config"] + ("_subset" if man.get("op") == "subset" else "")
+        out = os.path.join(REPO, "profiles", f"pmc_{tag}_v{m['variant']}o{m['tile_order']}_{args.round}.json")
         if os.path.exists(out) and not args.overwrite:
             print("keep", out)
             continue
@@ -115,6 +118,8 @@ def main():
     ap.add_argument("--warm", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--summarise", action="store_true")
+    ap.add_argument("--op", default="build", choices=["build", "subset"],
+                    help="subset: the GenerateDoG_nomp_dynamic build (bench.py --op subset)")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--round", default="r02")
