@@ -7,6 +7,7 @@ interface (gausspyramid.GaussPyramid) plus the batched / multi-GPU drivers.  The
 is not a Python identifier; load it with __graft_entry__.load_package().
 """
 from ._lib import GdpError, header_functions, lib  # noqa: F401
-from .gausspyramid import GaussPyramid, PyramidContext, conv_taps, octaves_for  # noqa: F401
+from .gausspyramid import (GaussPyramid, GaussPyramid_a512omp, GaussPyramid_a512xp, PyramidContext,  # noqa: F401
+                           conv_taps, octaves_for)
 
-__all__ = ["GdpError", "GaussPyramid", "PyramidContext", "conv_taps", "octaves_for", "lib", "header_functions"]
+__all__ = ["GdpError", "GaussPyramid", "GaussPyramid_a512omp", "GaussPyramid_a512xp", "PyramidContext", "conv_taps", "octaves_for", "lib", "header_functions"]

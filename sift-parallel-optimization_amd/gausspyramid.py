@@ -457,3 +457,59 @@ class GaussPyramid:
     def close(self):
         if getattr(self, "_ctx", None) is not None:
             self._ctx.close()
+
+
+class GaussPyramid_a512omp(GaussPyramid):
+    """GPU mirror of `class GaussPyramid_a512omp` (GaussDePyramid-AVX512xOpenMP.h:20-48), the
+    reference's timed AVX-512 x OpenMP path; same object model as GaussPyramid (include/
+    GaussDePyramid-HIP-AVX512.h is the C++ form).  Window centre: that header's integer length."""
+
+    counnt = 2  # GaussDePyramid-AVX512xOpenMP.h:18 (a global there; no effect on the GPU)
+
+    def __init__(self, img=None, len=None, S=2, device=0):  # noqa: A002
+        super().__init__(img, len, S, device)
+        if img is not None:
+            self._ctx.set_window_centre("intlen")
+
+    def GaussFilter(self, theLayer):
+        """:128-181 — the reference's body is commented out: nothing happens."""
+
+    def GenerateDoG(self):
+        """:183-213 — DoG pass only (level j -= level j+1, j = 0..S+1) per octave, twice on octaves
+        of side <= 2."""
+        for o in range(self.layer):
+            self._ctx.dog_octave(o)
+            if self.length >> o <= 2:
+                self._ctx.dog_octave(o)
+        self._fresh = False
+        self._cache.clear()
+
+    def GenerateDoG_nomp_dynamic(self):
+        """:240-364 — scales 0..S-1 windowed, DoG for i < S-1: {DoG_0..DoG_{S-2}, G_{S-1}, x, x, x}."""
+        if self._fresh:
+            self._ctx.build_subset()
+        else:
+            self._ctx.generate_dog_subset()
+        self._fresh = False
+        self._cache.clear()
+
+    def GenerateDoG_nomp_static(self):
+        """:366-368 — empty in the reference."""
+
+
+class GaussPyramid_a512xp(GaussPyramid):
+    """GPU mirror of `class GaussPyramid_a512xp` (GaussDePyramid-AVX512xPTHREAD.h:21-40): full
+    semantics; GenerateDoG with that header's integer-length centre (:193, :218), GaussFilter with
+    the serial float-halved one (:113-141)."""
+
+    def __init__(self, img=None, len=None, S=2, device=0):  # noqa: A002
+        super().__init__(img, len, S, device)
+        if img is not None:
+            self._ctx.set_window_centre("intlen")
+
+    def GaussFilter(self, theLayer):
+        self._ctx.set_window_centre("serial")
+        try:
+            super().GaussFilter(theLayer)
+        finally:
+            self._ctx.set_window_centre("intlen")

@@ -1147,3 +1147,31 @@ def test_cpp_a512_dropin_classes_match_reference(oracle, tmp_path):
     assert ran >= 15
     timing = subprocess.run([exe], check=True, timeout=120, capture_output=True, text=True).stdout.splitlines()
     assert len(timing) == 2 and all(float(t.split()[0]) > 0 for t in timing), timing
+
+
+def test_python_a512_mirrors_match_reference(pkg, oracle):
+    """The Python mirrors GaussPyramid_a512omp / GaussPyramid_a512xp (same names as the reference
+    classes) == the reference headers' output (a512_hashes.json), re-entry included, and
+    GaussPyInit restores the fused path."""
+    cls = {"GaussPyramid_a512omp::GenerateDoG_nomp_dynamic": (pkg.GaussPyramid_a512omp, "GenerateDoG_nomp_dynamic"),
+           "GaussPyramid_a512omp::GenerateDoG": (pkg.GaussPyramid_a512omp, "GenerateDoG"),
+           "GaussPyramid_a512xp::GenerateDoG": (pkg.GaussPyramid_a512xp, "GenerateDoG")}
+    ran = 0
+    for method, (C, name) in cls.items():
+        for rec in _a512_records(method):
+            n, S, spec, calls = rec["n"], rec["S"], rec["input"], rec["calls"]
+            if spec.startswith("synth:") or n > 1024:
+                continue
+            g = C(oracle.image_from_spec(n, spec), n, S)
+            try:
+                for _ in range(calls):
+                    getattr(g, name)()
+                _assert_hashes(oracle, g.pyramid(), rec, ("python", method))
+                g.GaussPyInit()
+                for _ in range(calls):
+                    getattr(g, name)()
+                _assert_hashes(oracle, g.pyramid(), rec, ("python after GaussPyInit", method))
+            finally:
+                g.close()
+            ran += 1
+    assert ran >= 15
