@@ -1175,3 +1175,28 @@ def test_python_a512_mirrors_match_reference(pkg, oracle):
                 g.close()
             ran += 1
     assert ran >= 15
+
+
+def test_subset_row_bands_reassemble_the_image(pkg, oracle):
+    """GenerateDoG_nomp_dynamic's subset on row-band contexts (the config-5 partition): fused and
+    in-place (re-entry) bands tile the whole image's subset output exactly."""
+    H, W, O, S = 512, 384, 5, 2
+    img = oracle.lcg_image(H, W, 21)
+    want = oracle.init_pyramid(img, S, O)
+    oracle.subset_a512omp(want, H, W, S, O)
+    oracle.subset_a512omp(want, H, W, S, O)
+    want = oracle.levels(want, H, W, S, O)
+    got = {k: np.zeros_like(v) for k, v in want.items()}
+    bands = [0, 128, 256, 512]
+    for r0, r1 in zip(bands[:-1], bands[1:]):
+        with pkg.PyramidContext(H, W, S=S, octaves=O, row_begin=r0, row_end=r1) as ctx:
+            ctx.set_window_centre("intlen")
+            ctx.set_input(img[r0:r1])
+            ctx.build_subset()
+            ctx.generate_dog_subset()
+            for o in range(O):
+                rows, cols, first = ctx.level_dims(o)
+                for s in range(S + 3):
+                    got[(o, s)][first:first + rows] = ctx.level(0, o, s)
+    for k in want:
+        _assert_same(got[k], want[k], ("subset band", k))
