@@ -95,6 +95,62 @@ def test_randomized_parity_sweep(pkg, oracle):
                 assert bad.size == 0, (what, b, bad[:5])
 
 
+# ---- GenerateDoG_nomp_dynamic's subset (the AVX-512 x OpenMP header's semantics) ----------------
+N_SUBSET_CASES = 120
+
+
+def test_randomized_subset_sweep(pkg, oracle):
+    """gdp_build_subset (+ a re-entry gdp_generate_dog_subset in half the cases) over the same random
+    shapes / S / octave counts / batches / formats / variants / tile orders / row bands, against
+    the oracle's restatement (pinned to the header run here by tests/test_oracle.py), with the
+    header's integer-length window centre."""
+    rng = np.random.default_rng(20261017)
+    for i in range(N_SUBSET_CASES):
+        H, W, S, O, B, fmt, _, variant, order, bands = _case(rng)
+        again = rng.random() < 0.5
+        imgs = _images(rng, H, W, B, fmt)
+        Oeff = O or oracle.default_octaves(H, W)
+        wants = []
+        for img in imgs:
+            w = oracle.init_pyramid(img.astype(np.int32), S, Oeff)
+            for _ in range(2 if again else 1):
+                oracle.subset_a512omp(w, H, W, S, Oeff)
+            wants.append(w)
+        what = dict(case=i, H=H, W=W, S=S, O=O, B=B, fmt=fmt, variant=variant, order=order, bands=bands, again=again)
+        if bands:
+            align = 1 << (max(Oeff, 5) - 1)
+            cuts = sorted({0, H} | {c for c in range(align, H, align) if rng.random() < 0.5})
+            want = oracle.levels(wants[0], H, W, S, Oeff)
+            got = {k: np.zeros_like(v) for k, v in want.items()}
+            for r0, r1 in zip(cuts[:-1], cuts[1:]):
+                with pkg.PyramidContext(H, W, S=S, octaves=O, row_begin=r0, row_end=r1, input_format=fmt) as ctx:
+                    ctx.set_tuning(variant=variant, tile_order=order)
+                    ctx.set_window_centre("intlen")
+                    ctx.set_input(imgs[0][r0:r1])
+                    ctx.build_subset()
+                    if again:
+                        ctx.generate_dog_subset()
+                    for o in range(Oeff):
+                        rows, cols, first = ctx.level_dims(o)
+                        for s in range(S + 3):
+                            if rows:
+                                got[(o, s)][first:first + rows] = ctx.level(0, o, s)
+            for k in want:
+                assert np.array_equal(_bits(got[k]), _bits(want[k])), (what, k)
+            continue
+        with pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, input_format=fmt) as ctx:
+            ctx.set_tuning(variant=variant, tile_order=order)
+            ctx.set_window_centre("intlen")
+            for b in range(B):
+                ctx.set_input(imgs[b], b)
+            ctx.build_subset()
+            if again:
+                ctx.generate_dog_subset()
+            for b in range(B):
+                bad = np.flatnonzero(_bits(ctx.pyramid(b)) != _bits(wants[b]))
+                assert bad.size == 0, (what, b, bad[:5])
+
+
 # ---- the convolution extension (no reference counterpart) -------------------------------------
 N_CONV_CASES = 120
 _CONV_TUNES = [dict(conv_kernel=2, conv_rows=32, conv_order=4), dict(conv_kernel=2, conv_rows=16, conv_order=0),
