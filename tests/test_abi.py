@@ -43,6 +43,11 @@ def test_host_only_entry_points(pkg):
     assert L.gdp_status_string(5) == b"no gfx950 device"
     assert L.gdp_device_level(None, 0, 0, 0) is None
     assert L.gdp_packed_floats(None) == 0
+    # every context-taking compute entry point rejects a null context with GDP_ERR_ARG, no GPU needed
+    for fn in ("gdp_build", "gdp_build_subset", "gdp_generate_dog", "gdp_generate_dog_subset", "gdp_init",
+               "gdp_build_gaussian", "gdp_sync"):
+        rc = L.gdp_sync(None) if fn == "gdp_sync" else getattr(L, fn)(None, None)
+        assert rc == 1, (fn, rc)
 
 
 def test_create_rejects_bad_arguments(pkg):
