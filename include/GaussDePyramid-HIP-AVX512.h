@@ -47,6 +47,9 @@ public:
     void GenerateDoG();
     void GenerateDoG_nomp_dynamic();
     void GenerateDoG_nomp_static() {}
+    // not members of the reference class (GaussPyramid_hip's MPI-variant entry points)
+    void GenerateDoG_mpi(int, char**) = delete;
+    void GenerateDoG_mgpu(int, char**) = delete;
 };
 
 inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
@@ -81,6 +84,8 @@ public:
     }
     // GenerateDoG: GaussPyramid_hip's (fused on fresh contents, else in place) with this
     // context's integer-length centre
+    void GenerateDoG_mpi(int, char**) = delete;  // not members of the reference class
+    void GenerateDoG_mgpu(int, char**) = delete;
 };
 
 #endif  // SIFT_GAUSSDEPYRAMID_HIP_AVX512_H
