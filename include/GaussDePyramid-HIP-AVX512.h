@@ -61,10 +61,12 @@ inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
 }
 
 inline void GaussPyramid_a512omp_hip::GenerateDoG() {
-    for (int o = 0; o < layer; ++o) {
-        check_(ctx_, gdp_dog_octave(ctx_, o, nullptr), "GenerateDoG");
-        if ((length >> o) <= 2) check_(ctx_, gdp_dog_octave(ctx_, o, nullptr), "GenerateDoG");
-    }
+    // per octave (:183-201): the DoG pass, then once more where the side is <= 2 — as two
+    // launches, all octaves and then the tiny ones
+    int tiny = 0;
+    while (tiny < layer && (length >> tiny) > 2) ++tiny;
+    check_(ctx_, gdp_dog_range(ctx_, 0, layer, nullptr), "GenerateDoG");
+    if (tiny < layer) check_(ctx_, gdp_dog_range(ctx_, tiny, layer, nullptr), "GenerateDoG");
     fresh_ = false;
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG");
     if (mirror_host) SyncHost();

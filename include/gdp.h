@@ -130,6 +130,8 @@ int gdp_gauss_range(gdp_ctx* ctx, int o_begin, int o_end, void* stream);
 /* DoG of octave o in place: level s -= level s+1 for s = 0..S+1 ascending
  * (GuassDePyramid.h:140-146). */
 int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);
+/* The DoG pass of every octave in [o_begin, o_end) in ONE launch (no window multiply). */
+int gdp_dog_range(gdp_ctx* ctx, int o_begin, int o_end, void* stream);
 /* GenerateDoG() in place on the CURRENT contents, all octaves in one launch
  * (GuassDePyramid.h:136-149).  After gdp_init this equals gdp_build; called again it re-filters,
  * like the reference's repeated-call timing loop (main.cpp:66-73). */

@@ -70,6 +70,7 @@ SIGNATURES = {
     "gdp_gauss_octave": (_c_int, [_p, _c_int, _p]),
     "gdp_gauss_range": (_c_int, [_p, _c_int, _c_int, _p]),
     "gdp_dog_octave": (_c_int, [_p, _c_int, _p]),
+    "gdp_dog_range": (_c_int, [_p, _c_int, _c_int, _p]),
     "gdp_generate_dog": (_c_int, [_p, _p]),
     "gdp_build_subset": (_c_int, [_p, _p]),
     "gdp_generate_dog_subset": (_c_int, [_p, _p]),

@@ -968,6 +968,12 @@ int gdp_dog_octave(gdp_ctx* c, int o, void* stream) try {
     return launch_inplace<2>(c, o, o + 1, c->pick(stream));
 } GDP_ABI_CATCH(c)
 
+int gdp_dog_range(gdp_ctx* c, int ob, int oe, void* stream) try {
+    if (!c || ob < 0 || oe > c->geom.O || ob >= oe) return c ? c->status(GDP_ERR_ARG, "octave range invalid") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<2>(c, ob, oe, c->pick(stream));
+} GDP_ABI_CATCH(c)
+
 int gdp_generate_dog(gdp_ctx* c, void* stream) try {
     if (!c) return GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));

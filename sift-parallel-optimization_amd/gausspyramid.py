@@ -217,6 +217,11 @@ class PyramidContext:
     def dog_octave(self, o, stream=None):
         check(lib().gdp_dog_octave(self._ctx, int(o), _stream_handle(stream)), self._ctx)
 
+    def dog_range(self, o_begin=0, o_end=None, stream=None):
+        """The DoG pass of octaves [o_begin, o_end) in one launch."""
+        o_end = self.O if o_end is None else o_end
+        check(lib().gdp_dog_range(self._ctx, int(o_begin), int(o_end), _stream_handle(stream)), self._ctx)
+
     def generate_dog(self, stream=None):
         check(lib().gdp_generate_dog(self._ctx, _stream_handle(stream)), self._ctx)
 
@@ -477,10 +482,10 @@ class GaussPyramid_a512omp(GaussPyramid):
     def GenerateDoG(self):
         """:183-213 — DoG pass only (level j -= level j+1, j = 0..S+1) per octave, twice on octaves
         of side <= 2."""
-        for o in range(self.layer):
-            self._ctx.dog_octave(o)
-            if self.length >> o <= 2:
-                self._ctx.dog_octave(o)
+        self._ctx.dog_range(0, self.layer)  # one launch for every octave ...
+        tiny = next((o for o in range(self.layer) if self.length >> o <= 2), self.layer)
+        if tiny < self.layer:
+            self._ctx.dog_range(tiny, self.layer)  # ... and one for the repeat on sides <= 2
         self._fresh = False
         self._cache.clear()
 

@@ -43,6 +43,8 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
     OK(gdp_generate_dog(c, nullptr));
     OK(gdp_checksum(c, 0, &again));
     EXPECT(built == again);
+    OK(gdp_dog_range(c, 0, go, nullptr));
+    EXPECT(gdp_dog_range(c, 1, 1, nullptr) == GDP_ERR_ARG);
     OK(gdp_build_subset(c, nullptr));  // GenerateDoG_nomp_dynamic fused, then in place
     OK(gdp_generate_dog_subset(c, nullptr));
     OK(gdp_sync(c));
