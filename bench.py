@@ -811,6 +811,12 @@ def main():
                                      f" [op={args.op}: in-place pass]")
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        result["cpu_baseline"]["semantics_vs_this_line"] = {
+            "build": "the GPU line computes the full GenerateDoG output; the timed CPU path its subset (see sample); "
+                     "serial_full_semantics / a512xp_full_semantics are the full-output CPU rates",
+            "subset": "identical: the GPU line computes GenerateDoG_nomp_dynamic's output",
+            "conv": "none: the reference has no convolution (the extension has no CPU counterpart)",
+        }.get(args.op, "in-place pass vs the CPU build path (different work)")
     elif rank == 0:
         result["cpu_baseline"] = None
     for c in ctxs:
