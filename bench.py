@@ -785,7 +785,7 @@ def main():
                         "gauss": "k_window (in-place row+column window, all octaves)",
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
                                  "240-column block tiles, one output row per wave, DPP lane shifts)" % ctx.tuning()["conv_rows"]
-                                 if ctx.tuning()["conv_kernel"] == 2 and S <= 3 else
+                                 if ctx.tuning()["conv_kernel"] == 2 and S <= 5 else
                                  "k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
                                  "DPP lane shifts, %d-row strips)" % ctx.tuning()["conv_rows"]
                                  if ctx.tuning()["conv_kernel"] == 0 and S <= 3 else

@@ -167,7 +167,7 @@ int gdp_conv_taps(int S, int scale, float* taps13, int* radius);
  * zero copy; pitch and image stride multiples of 4, rows 16-B aligned).  gdp_device_input returns
  * the device address and pitch of image b's input rows (the context's own or a bound buffer), the
  * rows a neighbour needs.  A band build fails with GDP_ERR_STATE until both halos it needs are
- * set, and only the block-tile kernel (GDP_TUNE_CONV_KERNEL 2, S <= 3, width a multiple of
+ * set, and only the block-tile kernel (GDP_TUNE_CONV_KERNEL 2, S <= 5, width a multiple of
  * 2^(octaves+1)) runs on bands; its output equals the whole image's rows bit for bit. */
 int gdp_conv_halo_rows(const gdp_ctx* ctx, int* above, int* below);
 int gdp_input_halo(gdp_ctx* ctx, int side /* 0 above, 1 below */, void** rows, size_t* pitch);
@@ -267,7 +267,7 @@ enum {
                                    (1 default, 2 or 4); 0 = one level per wave (k_levels_x) */
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (S <= 3), 1 LDS tiles,
-                                   2 block tiles (default; one output row per wave, S <= 3) */
+                                   2 block tiles (default; one output row per wave, S <= 5) */
     GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian: block tiles' rows per block (32 default;
                                    16 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8); the sweep's
                                    rows per wave strip (16 / 32) */

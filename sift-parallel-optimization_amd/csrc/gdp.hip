@@ -892,9 +892,9 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     const Geom& g = c->geom;
     const bool band = g.in_row0 != 0 || g.in_rows != g.H;
     if (band) {  // row band: only the block tiles read halo rows (every octave through them)
-        if (c->conv_kernel != 2 || g.L < 3 || g.L > 6)
+        if (c->conv_kernel != 2 || g.L < 3 || g.L > 8)
             return c->status(GDP_ERR_STATE, "gdp_build_gaussian on a row band runs the block tiles only "
-                                            "(GDP_TUNE_CONV_KERNEL 2, S <= 3)");
+                                            "(GDP_TUNE_CONV_KERNEL 2, S <= 5)");
         const int rc = conv_band_check(c);
         if (rc != GDP_OK) return rc;
     }
@@ -909,9 +909,10 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
         GDP_HIP(c, hipMemcpy(c->d_cradius, r.data(), r.size() * 4, hipMemcpyHostToDevice));
     }
     const hipStream_t st = c->pick(stream);
-    // the register sweep is compiled for S = 0..3 (L = 3..6) and takes the octaves whose width is a
-    // multiple of 4; the LDS tiles take the rest (and everything for other S or conv_kernel = 1)
-    const bool sweep = c->conv_kernel != 1 && g.L >= 3 && g.L <= 6;
+    // the block tiles (kernel 2) are compiled for S = 0..5 (L = 3..8), the register sweep (kernel
+    // 0) for S = 0..3; both take the octaves whose width is a multiple of 4, the LDS tiles the rest
+    // (and everything for other S or conv_kernel = 1)
+    const bool sweep = c->conv_kernel != 1 && g.L >= 3 && g.L <= (c->conv_kernel == 2 ? 8 : 6);
     {  // rows per tile / strip the selected kernel is instantiated for
         const int r = c->conv_rows, k = c->conv_kernel;
         const bool ok = k == 0 ? (r == 16 || r == 32) : true;
@@ -931,7 +932,9 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
                 case 3: GDP_HIP(c, launch_conv_sweep_l<3>(c, (unsigned)grid, st)); break;
                 case 4: GDP_HIP(c, launch_conv_sweep_l<4>(c, (unsigned)grid, st)); break;
                 case 5: GDP_HIP(c, launch_conv_sweep_l<5>(c, (unsigned)grid, st)); break;
-                default: GDP_HIP(c, launch_conv_sweep_l<6>(c, (unsigned)grid, st)); break;
+                case 6: GDP_HIP(c, launch_conv_sweep_l<6>(c, (unsigned)grid, st)); break;
+                case 7: GDP_HIP(c, launch_conv_blk<7>(c, (unsigned)grid, st)); break;
+                default: GDP_HIP(c, launch_conv_blk<8>(c, (unsigned)grid, st)); break;
             }
         }
     }

@@ -181,7 +181,7 @@ def test_randomized_convolution_sweep(pkg, oracle):
     """Seeded sweep of the convolution extension: shape 1..400 x 1..400, S 0..4, octave count,
     batch, int32 / uint8, every kernel / rows / waves / order the library has, against a float64
     convolution within the stated tolerance |err| <= 1e-3 + 1e-5 |ref|; and, when the width allows
-    (a multiple of 2^(O+1), S <= 3), a random row-band split whose bands — given their halo rows —
+    (a multiple of 2^(O+1), S <= 5), a random row-band split whose bands — given their halo rows —
     equal the whole image's build bit for bit."""
     import importlib
 
@@ -214,7 +214,17 @@ def test_randomized_convolution_sweep(pkg, oracle):
                 assert got.shape == ref.shape, what
                 assert (np.abs(got - ref) - (1e-3 + 1e-5 * np.abs(ref))).max() <= 0, (what, b, o, s)
         align = 1 << (max(O, 5) - 1)
-        if S <= 3 and W % (1 << (O + 1)) == 0 and H > 2 * align and rng.random() < 0.6:
+        if S <= 5 and W % (1 << (O + 1)) == 0 and H > 2 * align and rng.random() < 0.6:
+            band_tune = dict(conv_kernel=2, conv_rows=tune.get("conv_rows", 32) if tune.get("conv_kernel") == 2 else 32,
+                             conv_waves=tune.get("conv_waves", 16))
+            if tune.get("conv_kernel") != 2:  # bands run the block tiles: compare with the same kernel's whole image
+                with pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, input_format=fmt) as ctx:
+                    ctx.set_tuning(**band_tune)
+                    for b, im in enumerate(imgs):
+                        ctx.set_input(im, b)
+                    ctx.build_gaussian()
+                    ctx.sync()
+                    whole = {(b, o, s): ctx.level(b, o, s) for b in range(B) for o in range(O) for s in range(S + 3)}
             nb = int(rng.integers(2, max(3, H // align) + 1))
             for r in range(nb):
                 r0, r1 = d.plan_band(H, nb, r, O)
@@ -226,8 +236,7 @@ def test_randomized_convolution_sweep(pkg, oracle):
                 except ValueError:
                     plan_ok = False  # bands thinner than the halo: a band context still works locally
                 with pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, row_begin=r0, row_end=r1, input_format=fmt) as bc:
-                    bc.set_tuning(conv_kernel=2, conv_rows=tune.get("conv_rows", 32) if tune.get("conv_kernel") == 2 else 32,
-                                  conv_waves=tune.get("conv_waves", 16))
+                    bc.set_tuning(**band_tune)
                     for b, im in enumerate(imgs):
                         bc.set_input(np.ascontiguousarray(im[r0:r1]), b)
                     above, below = bc.conv_halo_rows()

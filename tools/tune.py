@@ -30,6 +30,7 @@ def main():
                     help="default op; a variant may override it with op=... (e.g. 'v=15;v=15,op=subset')")
     ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
     ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
+    ap.add_argument("--S", type=int, default=2, help="scales parameter S (S + 3 levels per octave)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
     ap.add_argument("--rotate", type=int, default=1,
                     help="buffer sets the timed launches cycle through (bench.py's cold-cache steps)")
@@ -39,7 +40,7 @@ def main():
     H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
     if args.shape:
         H, W, B = (int(x) for x in args.shape.split("x"))
-    ctxs = [pkg.PyramidContext(H, W, S=2, octaves=O, batch=B) for _ in range(args.rotate)]
+    ctxs = [pkg.PyramidContext(H, W, S=args.S, octaves=O, batch=B) for _ in range(args.rotate)]
     for c in ctxs:
         c.fill_synthetic(bench.SEED, 0)
         c.sync()
@@ -105,9 +106,9 @@ def main():
                 e1.synchronize()
                 times[name].append(e0.elapsed_time(e1) / args.iters)
     if args.op in ("build", "conv", "subset"):
-        nbytes = bench.algorithmic_bytes(H, W, 2, O, B)
+        nbytes = bench.algorithmic_bytes(H, W, args.S, O, B)
     else:
-        nbytes = 8 * 5 * B * sum((H >> o) * (W >> o) for o in range(O))
+        nbytes = 8 * (args.S + 3) * B * sum((H >> o) * (W >> o) for o in range(O))
     for name, _ in variants:
         t = np.array(times[name])
         print(json.dumps({"variant": name, "config": args.config, "shape": [H, W, B], "ms_median": round(float(np.median(t)), 5),
