@@ -586,6 +586,10 @@ def main():
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
+            # one-node rehearsal: gloo's pairs on loopback (otherwise gloo picks its interface by
+            # resolving this host's name, which this pool's boxes cannot always do)
+            if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+                os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
             dist.init_process_group(backend=backend)
     red_dev = "cuda" if backend == "nccl" else "cpu"
 

@@ -64,6 +64,7 @@ def _worker(rank, world, port, n, S, O, q):
     pkg = entry.load_package()
     oracle = entry.load_oracle()
     d = __import__(pkg.__name__ + ".distributed", fromlist=["x"])
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # loopback pairs: no host-name lookup
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         img = oracle.lcg_image(n, n, 12345)
@@ -118,6 +119,7 @@ def _scatter_worker(rank, world, port, per, q):
 
     pkg = entry.load_package()
     d = __import__(pkg.__name__ + ".distributed", fromlist=["x"])
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # loopback pairs: no host-name lookup
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         # rank 0 fills rank r's share with the synthetic images' generator stand-in r*1000 + i
@@ -230,6 +232,7 @@ def _halo_worker(rank, world, port, H, W, O, B, q):
 
     pkg = entry.load_package()
     d = __import__(pkg.__name__ + ".distributed", fromlist=["x"])
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # loopback pairs: no host-name lookup
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         full = torch.arange(B * H * W, dtype=torch.int32).reshape(B, H, W)
