@@ -272,6 +272,33 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
     return best[0], best[1], med[best]
 
 
+def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
+    """The in-place passes' block shape (GDP_TUNE_INPLACE_SUB / _WINDOW_SUB: 1024 / 512 / 256-thread
+    blocks, or k_levels_x) chosen like the build variant: every candidate timed over the ROTATED
+    cold step sequence, interleaved round-robin over `rounds`, median wins.  Bit-identical
+    outputs; the best shape depends on the workload (profiles/ab_regen_c*_r02ae.log)."""
+    import torch
+
+    times = {v: [] for v in values}
+    for _ in range(rounds):
+        for v in values:
+            for c in ctxs:
+                c.set_tuning(**{key: v})
+            for f in steps_fn:
+                f(stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(iters * len(ctxs)):
+                steps_fn[i % len(ctxs)](stream)
+            e1.record(stream)
+            e1.synchronize()
+            times[v].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
+    best = min(values, key=lambda v: sorted(times[v])[len(times[v]) // 2])
+    for c in ctxs:
+        c.set_tuning(**{key: best})
+    return best
+
+
 def scatter_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
     """SURVEY.md §8e's optional image-batch split, measured OUTSIDE the timed region: rank 0
     generates every rank's images (the same global indices the ranks otherwise generate locally),
@@ -688,6 +715,9 @@ def main():
             c.build(stream)  # materialise the pyramid the in-place passes work on
         steps_fn = [c.generate_dog if args.op == "regen" else (lambda st, c=c: c.gauss_range(0, O, st))
                     for c in ctxs]
+        if not args.no_autotune:
+            key, values = ("inplace_sub", [1, 4, 2, 0]) if args.op == "regen" else ("window_sub", [1, 4, 2])
+            autotuned = (key, autotune_inplace(ctxs, steps_fn, stream, 3 if B * H * W > (1 << 28) else 10, key, values))
     n_step = [0]
 
     def step(st):  # step i works on buffer set i mod rotate
@@ -785,8 +815,11 @@ def main():
                        "k_build<SUB> (fused decimate+window+DoG, GenerateDoG_nomp_dynamic's subset of levels), "
                        "variant %d, tile order %d" % (ctx.tuning()["variant"], ctx.tuning()["tile_order"])
                        if args.op == "subset" else
-                       {"regen": "k_levels<MODE=3> (in-place window+DoG, all octaves)",
-                        "gauss": "k_window (in-place row+column window, all octaves)",
+                       {"regen": ("k_levels_x (in-place window+DoG, one level per wave)" if tun["inplace_sub"] == 0 else
+                                  "k_levels<MODE=3> (in-place window+DoG, all octaves, %d-thread blocks)"
+                                  % (1024 // tun["inplace_sub"])) + (" (autotuned)" if autotuned else ""),
+                        "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks)%s"
+                                 % (1024 // tun["window_sub"], " (autotuned)" if autotuned else ""),
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
                                  "240-column block tiles, one output row per wave, DPP lane shifts)" % ctx.tuning()["conv_rows"]
                                  if ctx.tuning()["conv_kernel"] == 2 and S <= 5 else
