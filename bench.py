@@ -13,8 +13,9 @@ the 256 MB Infinity Cache between steps: the rate is the HBM rate.  One process 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 
 --gpus N > 1 without a launcher (WORLD_SIZE unset) starts N rank processes itself — one per GPU,
-RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment — before
-anything touches the GPU, and exits with the first failing rank's status; under torchrun
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 and a file rendezvous (GDP_BENCH_RDV) in
+their environment — before anything touches the GPU, and exits with the first failing rank's
+status; under torchrun
 (WORLD_SIZE set) it is one of the ranks.  A world size that differs from --gpus, or more ranks
 than visible GPUs under "nccl", is an error.
 
@@ -97,11 +98,12 @@ def cpu_baseline(budget_s):
     n, S = 4096, 2
     threads = host_threads()
     spec = f"synth:{SEED:#x}:0"
-    if oracle.ref_binary("avx512") and oracle.host_has_avx512():
+    have_bin, have_isa = oracle.ref_binary("avx512"), oracle.host_has_avx512()
+    if have_bin and have_isa:
         probe = oracle.ref_time("time-a512omp", n, S, spec, 2, threads)
         reps = max(3, min(400, int(budget_s / max(probe["ms_median"] / 1e3, 1e-4))))
         rec = oracle.ref_time("time-a512omp", n, S, spec, reps, threads)
-        serial = oracle.ref_time("time-serial", n, S, spec, 2) if oracle.ref_binary("serial") else None
+        serial = oracle.ref_time("time-serial", n, S, spec, 5) if oracle.ref_binary("serial") else None
         out = {
             "value": round(n * n / (rec["ms_median"] / 1e3) / 1e6, 3), "unit": "Mpix/s", "cores": threads,
             "kind": "reference",
@@ -111,6 +113,9 @@ def cpu_baseline(budget_s):
                        f"NB: that path filters only S of the S+3 scales and forms 1 of the S+2 DoG levels "
                        f"(~34% of the full build's bytes)"),
             "cpu": cpu_info(),
+            # which reference text the timed binary was compiled from: oracle/Makefile's stamp
+            # (sha256 of every source the compile read, compiler, flags; oracle/stamp.py)
+            "provenance": _ref_stamp(have_bin),
         }
         if serial:
             out["serial_full_semantics"] = {"value": round(n * n / (serial["ms_median"] / 1e3) / 1e6, 3),
@@ -129,6 +134,10 @@ def cpu_baseline(budget_s):
         return out
     import numpy as np
 
+    reason = ("oracle/_ref/ref_avx512 (the reference header compiled in place) is not in this tree"
+              if not have_bin else "this host's CPU lacks AVX-512F, which the reference header needs")
+    print(f"bench.py: cpu_baseline falls back to the oracle restatement (kind 'port'): {reason}",
+          file=sys.stderr, flush=True)
     img = oracle.synthetic_image(n, n, SEED, 0)
     base = oracle.init_pyramid(img, S)
     O = oracle.octaves(n)
@@ -141,8 +150,25 @@ def cpu_baseline(budget_s):
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
     return {"value": round(n * n / med / 1e6, 3), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "reason": reason,
             "sample": f"oracle restatement of GenerateDoG_nomp_dynamic (OpenMP, {threads} threads), {n}x{n}, "
                       f"median of {len(times)} calls", "cpu": cpu_info()}
+
+
+def _ref_stamp(binary):
+    """oracle/_ref/<binary>.stamp.json (written by `make -C oracle ref`), or why it is missing."""
+    try:
+        with open(binary + ".stamp.json") as f:
+            st = json.load(f)
+    except (OSError, ValueError, TypeError):
+        return {"status": "no stamp next to the binary (built before oracle/stamp.py existed): provenance unrecorded"}
+    import hashlib
+
+    with open(binary, "rb") as f:
+        actual = hashlib.sha256(f.read()).hexdigest()
+    return {"binary_sha256": st.get("binary_sha256"), "binary_matches_stamp": actual == st.get("binary_sha256"),
+            "sources_sha256": {os.path.basename(k): v for k, v in st.get("sources", {}).items()},
+            "compiler": st.get("compiler"), "flags": st.get("flags"), "built_utc": st.get("built_utc")}
 
 
 def latest_conv_pmc(config_key, tun):
@@ -189,22 +215,59 @@ def latest_pmc(config_key, variant, tile_order, op="build", levels=5):
     return best
 
 
+def latest_inplace_pmc(config_key, op, tun):
+    """PMC record of an in-place pass (--op regen: k_levels<MODE 3> / k_levels_x, keyed by
+    GDP_TUNE_INPLACE_SUB; --op gauss: k_window, keyed by GDP_TUNE_WINDOW_SUB) with the run's block
+    shape, or None."""
+    key = "inplace_sub" if op == "regen" else "window_sub"
+    pdir = os.path.join(REPO, "profiles")
+    best = None
+    for f in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
+        if f.startswith("pmc_") and f.endswith(".json"):
+            try:
+                with open(os.path.join(pdir, f)) as fh:
+                    rec = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if rec.get("config") == config_key and rec.get("op") == op and rec.get("kernel_bytes_per_launch") and \
+                    rec.get(key) == tun[key]:
+                best = dict(rec, file=f)
+    return best
+
+
 def launch_ranks(n, argv, script=None):
     """`bench.py --gpus N` with no launcher: start N rank processes of this script (one per GPU)
     and wait for them.  Runs before anything imports torch or touches the GPU; the parent never
-    does.  If a rank fails the others are stopped (they would wait in a collective forever)."""
-    import signal
-    import socket
-    import subprocess
+    does.  If a rank fails the others are stopped (they would wait in a collective forever).
 
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    procs = []
+    Rendezvous: a FILE in a fresh private directory (GDP_BENCH_RDV, torch.distributed's file://
+    init method), not a TCP port.  Round 2 picked MASTER_PORT by binding port 0 and closing the
+    socket before the children bound it: between the close and rank 0's TCPStore bind the port was
+    free for anyone — another process's bind, or (the port is in the ephemeral range) a rank's own
+    TCPStore client connect() retrying on 127.0.0.1:P while rank 0 was still importing torch, which
+    the kernel can complete as a TCP self-connect (source port == P), so the client reads its own
+    request back.  A file rendezvous has no port to lose.
+
+    Each rank's stderr also goes to <GDP_BENCH_RANK_LOGS>/rank<r>.stderr when that directory is
+    set (tests keep it); a failing rank's tail is printed with the path either way."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+
+    rdv_dir = tempfile.mkdtemp(prefix="gdp_bench_rdv_")
+    log_dir = os.environ.get("GDP_BENCH_RANK_LOGS") or rdv_dir
+    os.makedirs(log_dir, exist_ok=True)
+    procs, logs = [], []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env))
+                   MASTER_ADDR="127.0.0.1", GDP_BENCH_RDV=os.path.join(rdv_dir, "rendezvous"))
+        env.pop("MASTER_PORT", None)
+        path = os.path.join(log_dir, f"rank{r}.stderr")
+        logs.append(path)
+        with open(path, "wb") as err:
+            procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env,
+                                          stderr=err))
     rc = 0
     try:
         live = list(procs)
@@ -216,8 +279,14 @@ def launch_ranks(n, argv, script=None):
                 live.remove(p)
                 if code != 0 and rc == 0:
                     rc = code if code > 0 else 128 - code
-                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
-                          file=sys.stderr, flush=True)
+                    r = procs.index(p)
+                    try:
+                        with open(logs[r], "rb") as f:
+                            tail = f.read()[-4000:].decode(errors="replace")
+                    except OSError:
+                        tail = "(stderr log unreadable)"
+                    print(f"bench.py: rank {r} exited with {code}; stopping the other ranks. Its stderr "
+                          f"({logs[r]}), last 4000 bytes:\n{tail}", file=sys.stderr, flush=True)
                     for q in live:
                         q.send_signal(signal.SIGTERM)
             time.sleep(0.05)
@@ -229,7 +298,50 @@ def launch_ranks(n, argv, script=None):
                 except subprocess.TimeoutExpired:
                     p.kill()
                     p.wait()
+        if rc == 0:  # a passing rank's stderr (warnings) still reaches the caller
+            for path in logs:
+                try:
+                    with open(path, "rb") as f:
+                        sys.stderr.write(f.read().decode(errors="replace"))
+                except OSError:
+                    pass
+        shutil.rmtree(rdv_dir, ignore_errors=True)
     return rc
+
+
+def rank_topology(world, rank, local, backend, dist, args):
+    """Which device each rank drives, and how many ranks the collective backend sees — so an
+    N-rank line proves "N ranks on N distinct GPUs" from its own record: every rank's device
+    ordinal, PCI address and UUID (all_gather_object), and an all_reduce of ones over the process
+    group (RCCL under "nccl": `rccl_world`).  Under nccl a shared device or a count other than
+    --gpus is fatal (before any timing); a gloo rehearsal records its shared device explicitly."""
+    import torch
+
+    props = torch.cuda.get_device_properties(local)
+    me = {"rank": rank, "device": local, "name": props.name,
+          "pci": "%04x:%02x:%02x.0" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", 0),
+                                        getattr(props, "pci_device_id", 0)),
+          "uuid": str(getattr(props, "uuid", "")),
+          "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES", os.environ.get("CUDA_VISIBLE_DEVICES"))}
+    if dist is None:
+        return {"backend": None, "collective_world": 1, "devices": [me], "distinct_devices": 1}
+    devs = [None] * world
+    dist.all_gather_object(devs, me)
+    ones = torch.ones(1, dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(ones)
+    counted = int(ones.item())
+    ids = {(d["pci"], d["uuid"]) for d in devs}
+    topo = {"backend": "rccl" if backend == "nccl" else backend, "collective_world": counted, "devices": devs,
+            "distinct_devices": len(ids)}
+    if backend == "nccl":
+        topo["rccl_world"] = counted
+        if counted != args.gpus or len(ids) != world:
+            sys.exit(f"bench.py: RCCL counted {counted} ranks on {len(ids)} distinct devices for --gpus {args.gpus}: "
+                     f"{devs}")
+    else:
+        topo["note"] = (f"{backend} rehearsal: {world} ranks on {len(ids)} device(s) — not a multi-GPU measurement"
+                        if len(ids) < world else f"{backend} ranks on distinct devices")
+    return topo
 
 
 def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
@@ -520,6 +632,50 @@ def verify(ctx, cfg, key, world, rank, dist, mg, first_image, subset=False):
                         "oracle closed form (non-square input: no reference output exists)")}
 
 
+INPLACE_CALLS = {"regen": 3, "gauss": 2}  # checksums_inplace.json's K per op
+
+
+def verify_inplace(ctx, cfg, op, stream, world, rank, dist, mg, first_image):
+    """The in-place passes (--op regen: GenerateDoG re-entry, main.cpp:66-73's loop; --op gauss:
+    GaussFilter of every octave) after the timed region, with the timed kernel instance: rotated
+    set 0 is refilled (gdp_init = GaussPyInit) and K calls of the op run on it; the first and last
+    image of every rank are then checksummed against the serial reference's output after the same
+    K calls on the same input (tests/golden/checksums_inplace.json, oracle/_ref/ref_serial
+    regen/gauss).  Image configs only (no fixture of the 16384^2 or non-square re-entry)."""
+    K = INPLACE_CALLS[op]
+    H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
+    ctx.init(stream)
+    for _ in range(K):
+        if op == "regen":
+            ctx.generate_dog(stream)
+        else:
+            ctx.gauss_range(0, O, stream)
+    stream.synchronize()
+    fixtures = {}
+    with open(os.path.join(REPO, "tests", "golden", "checksums_inplace.json")) as f:
+        for r in json.load(f):
+            if r["op"] == op and r["calls"] == K and r["n"] == H == W and r["S"] == 2 and f"octaves_{O}" in r and \
+                    r["input"].lower().startswith(f"synth:{SEED:#x}:".lower()):
+                fixtures[int(r["input"].split(":")[2])] = int(r[f"octaves_{O}"], 16)
+    local = sorted({0, B - 1})
+    mine = [v for b in local for v in (first_image + b, ctx.checksum(b))]
+    per_rank = mg.gather_checksums(mine, dist=dist)
+    if rank != 0:
+        return None
+    checked, bad, unchecked = [], [], []
+    for flat in per_rank:
+        for idx, got in zip(flat[0::2], flat[1::2]):
+            want = fixtures.get(int(idx))
+            (unchecked if want is None else checked if got == want else bad).append(int(idx))
+    return {"status": "MISMATCH" if bad else ("bit-exact" if checked else "unchecked (no fixture for these images)"),
+            "checked": f"GaussPyInit + {K} x {'GenerateDoG' if op == 'regen' else 'GaussFilter(every octave)'} "
+                       f"after the timed region, same kernel instance; first and last image of each of {world} "
+                       f"rank(s): global images {sorted(checked + bad)}",
+            "against": "reference output (tests/golden/checksums_inplace.json: oracle/_ref/ref_serial "
+                       f"{op} {K})", "bit_exact_images": len(checked), "mismatched_images": bad,
+            "images_without_fixture": unchecked, "post_timing_launches": K}
+
+
 def verify_conv_bands(ctx, cfg, world, rank, dist, mg, in_fmt):
     """Convolution extension on row bands (no reference output exists for this mode): the sum of
     every rank's band checksum must equal the checksum of the whole image built on ONE GPU (rank
@@ -558,6 +714,9 @@ def main():
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
+    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4],
+                    help="--op regen/gauss: force the in-place block shape (GDP_TUNE_INPLACE_SUB / _WINDOW_SUB: "
+                         "1024 / N threads, 0 = k_levels_x) and skip its autotune, e.g. for profiling runs")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
                     help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv", "subset"],
@@ -610,14 +769,18 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        # self-launched ranks meet through a file (launch_ranks); under torchrun, env:// as usual
+        rdv = os.environ.get("GDP_BENCH_RDV")
+        init = dict(init_method="file://" + rdv, rank=rank, world_size=world) if rdv else {}
         if backend == "nccl":
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local), **init)
         else:
             # one-node rehearsal: gloo's pairs on loopback (otherwise gloo picks its interface by
             # resolving this host's name, which this pool's boxes cannot always do)
             if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
                 os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-            dist.init_process_group(backend=backend)
+            dist.init_process_group(backend=backend, **init)
+    topology = rank_topology(world, rank, local, backend, dist, args)
     red_dev = "cuda" if backend == "nccl" else "cpu"
 
     cfg = dict(CONFIGS[args.config])
@@ -715,8 +878,13 @@ def main():
             c.build(stream)  # materialise the pyramid the in-place passes work on
         steps_fn = [c.generate_dog if args.op == "regen" else (lambda st, c=c: c.gauss_range(0, O, st))
                     for c in ctxs]
-        if not args.no_autotune:
-            key, values = ("inplace_sub", [1, 4, 2, 0]) if args.op == "regen" else ("window_sub", [1, 4, 2])
+        key, values = ("inplace_sub", [1, 4, 2, 0]) if args.op == "regen" else ("window_sub", [1, 4, 2])
+        if args.inplace_sub is not None:
+            if args.inplace_sub not in values:
+                sys.exit(f"bench.py: --inplace-sub {args.inplace_sub} is not a {key} value ({values})")
+            for c in ctxs:
+                c.set_tuning(**{key: args.inplace_sub})
+        elif not args.no_autotune:
             autotuned = (key, autotune_inplace(ctxs, steps_fn, stream, 3 if B * H * W > (1 << 28) else 10, key, values))
     n_step = [0]
 
@@ -746,12 +914,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
+    if dist:  # every rank's own timing, recorded beside the max that the line reports
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "ms_per_step": round(wall * 1e3 / args.steps, 6),
+                                          "kernel_ms": round(kernel_ms, 6)})
+        topology["per_rank"] = per_rank
     wall, kernel_ms = mg.max_over_ranks([wall, kernel_ms], dist=dist, device=red_dev)
     parity = (verify(ctx, cfg, args.config, world, rank, dist, mg, first_image, subset=args.op == "subset")
               if args.op in ("build", "subset") else None)
     if halo_exchange:
         parity = verify_conv_bands(ctx, cfg, world, rank, dist, mg, args.input)
-    if parity is not None and rotate > 1:
+    if args.op in ("regen", "gauss") and not cfg["band"]:
+        parity = verify_inplace(ctx, cfg, args.op, stream, world, rank, dist, mg, first_image)
+    if parity is not None and rotate > 1 and args.op not in ("regen", "gauss"):
         # every rotated set built the same images: their checksums must all equal set 0's
         sums = {c.checksum(0) for c in ctxs}
         parity["rotated_sets_agree"] = len(sums) == 1
@@ -777,6 +952,8 @@ def main():
            if args.op in ("build", "subset") and args.input == "i32" and not (cfg["band"] and world > 1) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
+    if args.op in ("regen", "gauss") and not (cfg["band"] and world > 1):
+        pmc = latest_inplace_pmc(args.config, args.op, tun)
 
     result = {
         "metric": METRIC,
@@ -807,6 +984,8 @@ def main():
             "traffic_source": (f"profiles/{pmc['file']}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same "
                                + (f"kernel instance (conv kernel {pmc['conv_kernel']}, rows {pmc['conv_rows']}, order "
                                   f"{pmc['conv_order']}) on this workload" if args.op == "conv" else
+                                  f"kernel instance (inplace_sub {pmc['inplace_sub']}) on this workload" if args.op == "regen" else
+                                  f"kernel instance (window_sub {pmc['window_sub']}) on this workload" if args.op == "gauss" else
                                   f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}) on this workload")
                                if pmc else "no PMC profile of this kernel instance (variant/tile order) on this workload"),
             "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d%s"
@@ -833,9 +1012,11 @@ def main():
             "algorithmic_bytes_per_launch": bytes_launch,
         },
     }
-    result["parity"] = parity if (args.op in ("build", "subset") or halo_exchange) else (
-        {"status": "extension: no reference output (tests/ check it against a float64 convolution)"}
-        if args.op == "conv" else {"status": "not checked for in-place re-entry ops"})
+    result["parity"] = parity if (args.op in ("build", "subset", "regen", "gauss") or halo_exchange) else (
+        {"status": "extension: no reference output (tests/ check it against a float64 convolution)"})
+    if result["parity"] is None:  # an in-place op on the row-band config
+        result["parity"] = {"status": "unchecked (no reference re-entry fixture of this workload)"}
+    result["topology"] = topology
     if distribution is not None:
         result["distribution"] = distribution
     if collect is not None:

@@ -1,8 +1,10 @@
 // The reference's driver (main.cpp:26-75) with the one-line include / class-name swap that the
 // drop-in boundary promises: all-ones MAX x MAX image, n = 512, S = 2, GenerateDoG timed in a
 // loop until >= 100 ms, mean ms printed.  Extra (optional) arguments make it a parity tool:
-//     main_hip [n] [S] [input: ones | lcg:SEED] [dump.f32] [calls]
-// writes the pyramid after `calls` GenerateDoG() calls in the packed [o][s][r][c] layout.
+//     main_hip [n] [S] [input: ones | lcg:SEED] [dump.f32] [calls] [dog | mpi | mixed]
+// writes the pyramid after `calls` GenerateDoG() calls (`mpi`: GenerateDoG_mpi(argc, argv) calls,
+// main.cpp:68's method; `mixed`: GenerateDoG_mpi, GenerateDoG, GenerateDoG_mpi, ...) in the packed
+// [o][s][r][c] layout.
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -39,8 +41,14 @@ int main(int argc, char* argv[]) {
     }
     if (argc > 4) {  // parity mode
         const int calls = argc > 5 ? std::atoi(argv[5]) : 1;
+        const std::string mode = argc > 6 ? argv[6] : "dog";
         GaussPyramid_hip g(p, n, S);
-        for (int c = 0; c < calls; ++c) g.GenerateDoG();
+        for (int c = 0; c < calls; ++c) {
+            if (mode == "mpi" || (mode == "mixed" && c % 2 == 0))
+                g.GenerateDoG_mpi(argc, argv);
+            else
+                g.GenerateDoG();
+        }
         FILE* f = std::fopen(argv[4], "wb");
         int len = n;
         for (int o = 0; o < gdp_octaves_for(n); ++o, len /= 2)

@@ -79,7 +79,8 @@ public:
         check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GaussPyramid_a512xp_hip");
     }
     void GaussFilter(int theLayer) {
-        // the serial header's float-halved centre for this method only (:113-141)
+        // the serial header's float-halved centre for this method only (:113-141); each centre
+        // has its own device tap table, so the two switches are pointer swaps (no drain/upload)
         check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_SERIAL), "GaussFilter");
         GaussPyramid_hip::GaussFilter(theLayer);
         check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GaussFilter");

@@ -49,8 +49,13 @@ public:
     void GenerateDoG();
     // GaussPyramid_mpi::GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335), the call main.cpp:68 makes.
     // The reference fans scales out over >= S+4 MPI ranks and collects on rank S+3; here one GPU
-    // does the whole pyramid, so the result every caller sees is the collector's.  Unlike the
-    // reference (MPI_Init/MPI_Finalize inside) it may be called any number of times.
+    // does the whole pyramid and GaussPy ends as that collector's GaussPy.  Like the method it
+    // replaces, it centres every window on the INTEGER octave length (`l = float(len - 1) / 2.0`,
+    // :273 — GDP_CENTRE_INTLEN), not on the float-halved length GaussFilter/GenerateDoG use
+    // (:133-183, GuassDePyramid.h:107-115); the two differ when n is not a multiple of
+    // 2^(layer-1) (n = 100, 1000, ...).  The context returns to the serial centre afterwards, so
+    // GaussFilter/GenerateDoG keep theirs.  Unlike the reference (MPI_Init/MPI_Finalize inside)
+    // it may be called any number of times; each call continues from the current contents.
     void GenerateDoG_mpi(int argc, char** argv);
     void GenerateDoG_mgpu(int argc, char** argv) { GenerateDoG_mpi(argc, argv); }  // SURVEY §8(f2) name
     ~GaussPyramid_hip();
@@ -137,7 +142,17 @@ inline void GaussPyramid_hip::GenerateDoG() {
     if (mirror_host) SyncHost();
 }
 
-inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) { GenerateDoG(); }
+inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
+    // switching centres selects the other device tap table (no drain, no re-upload after the
+    // first call); both calls below are ordered on the context's stream
+    check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi");
+    const int rc = fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr);
+    check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi");
+    check_(ctx_, rc, "GenerateDoG_mpi");
+    fresh_ = false;
+    check_(ctx_, gdp_sync(ctx_), "GenerateDoG_mpi");
+    if (mirror_host) SyncHost();
+}
 
 inline void GaussPyramid_hip::output() {  // :89-104
     int len = length;

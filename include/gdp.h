@@ -162,7 +162,8 @@ int gdp_conv_taps(int S, int scale, float* taps13, int* radius);
  * up to 6 * 2^(octaves-1) input rows above and below it (clipped to the image): *above / *below
  * (0 for whole-image contexts).  A band's gdp_build_gaussian reads them from halo buffers
  * [batch][rows][pitch] (the context's input format): the context's own (gdp_input_halo allocates
- * one on first call and returns its device address, for a neighbour's rows to be written into —
+ * one on first call, binds it and returns its device address — later calls only return it, with
+ * no geometry upload — for a neighbour's rows to be written into —
  * gdp_comm_exchange_halo over RCCL, or any copy) or caller device memory (gdp_bind_input_halo,
  * zero copy; pitch and image stride multiples of 4, rows 16-B aligned).  gdp_device_input returns
  * the device address and pitch of image b's input rows (the context's own or a bound buffer), the
@@ -238,8 +239,10 @@ int gdp_get_taps(gdp_ctx* ctx, int axis, int octave, int scale, float* host);
  * c = float(len_o - 1) / 2 with the INTEGER length len_o = n >> o, what the multi-process variants
  * compute (GaussPyramid_mpi::GenerateDoG_mpi, GaussDePyramid-MPI.h:273; mpitest.cpp:44,123).  The
  * two agree bit for bit whenever every octave's float length is whole (n a multiple of
- * 2^(octaves-1)); they differ for e.g. n = 100 from octave 3 on.  Re-uploads the tap tables
- * (drains the device first).  Pure layout of the taps: kernels and bytes are unchanged. */
+ * 2^(octaves-1)); they differ for e.g. n = 100 from octave 3 on.  Each mode has its own device
+ * tap table, built and uploaded on its first use (a blocking copy); after that a switch only
+ * selects the table the NEXT launch reads — no device drain, launches already queued keep the
+ * table they were launched with.  Pure layout of the taps: kernels and bytes are unchanged. */
 enum { GDP_CENTRE_SERIAL = 0, GDP_CENTRE_INTLEN = 1 };
 int gdp_set_window_centre(gdp_ctx* ctx, int mode);
 int gdp_get_window_centre(const gdp_ctx* ctx);
@@ -250,7 +253,10 @@ int gdp_get_window_centre(const gdp_ctx* ctx);
  * exactly its rows of the whole pyramid's CURRENT contents, so an in-place call on the band
  * (gdp_generate_dog, gdp_gauss_octave, ...) continues where the whole image left off (the
  * operation is pointwise).  Device-to-device, ordered on `stream` (NULL = the band's stream),
- * blocking.  Used by the MPI drop-in to re-enter GenerateDoG_mpi after single-process calls. */
+ * blocking.  Before copying it waits for `full`'s OWN stream only: work the caller queued for
+ * `full` on any other stream must be complete (or ordered before `stream`) when this is called.
+ * (The C++ MPI drop-in does not use it: after single-process calls each rank re-enters on its
+ * whole-image context instead, GaussDePyramid-HIP-mpi.h.) */
 int gdp_copy_band(gdp_ctx* band, int band_image, const gdp_ctx* full, int full_image, void* stream);
 
 /* ---- tuning (performance only; results are bit-identical for every setting) --------------- */

@@ -85,7 +85,10 @@ int gdp_comm_halo_plan(int height, int nranks, int rank, int octaves, gdp_halo_t
  * ncclGroupStart/End.  `band` must be gdp_band_rows' band of this rank (NULL on a rank whose band
  * is empty), its input pitch the width rounded up to 4 (the owned input, or a bound input of that
  * pitch).  Stream-ordered on `stream` (NULL = the band's stream); returns when enqueued (the
- * following gdp_build_gaussian on the same stream sees the rows). */
+ * following gdp_build_gaussian on the same stream sees the rows).  The FIRST call on a band
+ * allocates and binds its halo buffers (gdp_input_halo: a blocking geometry upload that drains the
+ * device); every later call only enqueues the transfers.  A failure returns the status of the
+ * step that failed (GDP_ERR_NOMEM only for an allocation). */
 int gdp_comm_exchange_halo(gdp_comm* comm, gdp_ctx* band, void* stream);
 
 #ifdef __cplusplus

@@ -11,6 +11,8 @@
 //   ref_harness taps   <n> <S> <out.f32>                   reference `filter` taps for every (o, s)
 //   ref_harness regen  <n> <S> <input> <calls> <out.f32>   GenerateDoG() called <calls> times
 //   ref_harness regen-hash <n> <S> <input> <calls>         per-level FNV hashes of the same
+//   ref_harness gauss  <n> <S> <input> <calls> <out.f32>   GaussFilter(o) of every octave, <calls>
+//                                                          rounds, on the constructor's GaussPyInit
 //   ref_harness dump-a512omp <n> <S> <input> <out.f32>     GenerateDoG_nomp_dynamic() output
 //   ref_harness dump-a512xp  <n> <S> <input> <out.f32>     GaussPyramid_a512xp::GenerateDoG() output
 //   ref_harness hash-a512omp <n> <S> <input> <calls> <method> [threads]  per-level FNV hashes after
@@ -129,6 +131,12 @@ int main(int argc, char** argv) {
         GaussPyramid g(img, n, S);
         const int calls = std::atoi(argv[5]);
         for (int c = 0; c < calls; ++c) g.GenerateDoG();
+        dump(g.GaussPy, n, S, argv[6]);
+    } else if (mode == "gauss") {
+        GaussPyramid g(img, n, S);
+        const int calls = std::atoi(argv[5]);
+        for (int c = 0; c < calls; ++c)
+            for (int o = 0; o < octaves_of(n); ++o) g.GaussFilter(o);
         dump(g.GaussPy, n, S, argv[6]);
 #ifdef WITH_AVX512
     } else if (mode == "dump-a512omp") {

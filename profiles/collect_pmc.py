@@ -46,10 +46,17 @@ def main():
     ap.add_argument("--bench-json", help="bench.py output line of the traced run (optional)")
     ap.add_argument("--kernel", default="k_build", help="substring of the kernel to summarise")
     ap.add_argument("--op", default="build", help="bench.py --op of the profiled run")
-    ap.add_argument("--variant", type=int, required=True, help="build variant the profiled runs were forced to")
-    ap.add_argument("--tile-order", type=int, required=True, help="build tile order of the profiled runs")
+    ap.add_argument("--variant", type=int, default=None, help="build variant the profiled runs were forced to")
+    ap.add_argument("--tile-order", type=int, default=None, help="build tile order of the profiled runs")
+    ap.add_argument("--inplace-sub", type=int, default=None,
+                    help="--op regen: GDP_TUNE_INPLACE_SUB the profiled runs were forced to (0 = k_levels_x)")
+    ap.add_argument("--window-sub", type=int, default=None, help="--op gauss: GDP_TUNE_WINDOW_SUB of the profiled runs")
     ap.add_argument("--tag", default=None, help="file tag (default: config, or config_op)")
     args = ap.parse_args()
+    if args.op in ("build", "subset") and (args.variant is None or args.tile_order is None):
+        ap.error("--op build/subset records need --variant and --tile-order")
+    if args.op == "regen" and args.inplace_sub is None or args.op == "gauss" and args.window_sub is None:
+        ap.error("--op regen needs --inplace-sub, --op gauss --window-sub")
 
     import bench
 
@@ -71,6 +78,8 @@ def main():
     rec = {
         "config": args.config, "round": args.round, "kernel": name,
         "variant": args.variant, "tile_order": args.tile_order, "input_format": "i32",
+        **({"inplace_sub": args.inplace_sub} if args.inplace_sub is not None else {}),
+        **({"window_sub": args.window_sub} if args.window_sub is not None else {}),
         "trace_calls": int(stats["Calls"]) if stats else None,
         "trace_avg_ns": float(stats["AverageNs"]) if stats else None,
         "trace_min_ns": float(stats["MinNs"]) if stats else None,
@@ -97,7 +106,9 @@ def main():
             durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
                     for r in sorted((r for r in csv.DictReader(f) if r["Kernel_Name"] == name),
                                     key=lambda r: int(r["Start_Timestamp"]))]
-        timed = durs[-int(line["steps"]):]
+        # launches of the same kernel after the timed region (the in-place ops' parity calls)
+        post = int((line.get("parity") or {}).get("post_timing_launches", 0))
+        timed = durs[-int(line["steps"]) - post:len(durs) - post]
         if timed:
             rec["trace_timed_steps"] = len(timed)
             rec["trace_timed_avg_ns"] = statistics.mean(timed)

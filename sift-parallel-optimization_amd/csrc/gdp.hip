@@ -91,7 +91,9 @@ struct gdp_ctx {
     void* d_halo_own[2] = {nullptr, nullptr}; // context-owned halo rows above / below a band (conv extension)
     const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
-    float* d_taps = nullptr;
+    float* d_taps = nullptr;      // the table the next launch reads: d_taps_mode[centre_mode]
+    float* d_taps_mode[2] = {nullptr, nullptr}; // one device tap table per window-centre mode, built on
+                                  // first use, so switching centres is a pointer swap (no drain)
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
     int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
@@ -245,15 +247,15 @@ int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     }
 }
 
-// Column taps of every (o, s) from W, row taps from H (aliased for square images), in the
-// context's window-centre mode (host memory only).
-void fill_host_taps(gdp_ctx* c) {
+// Column taps of every (o, s) from W, row taps from H (aliased for square images), in window-
+// centre mode `mode` (host memory only).
+void fill_host_taps(gdp_ctx* c, int mode) {
     const Geom& g = c->geom;
     for (int o = 0; o < g.O; ++o) {
         const OctGeom& og = g.oct[o];
         for (int s = 0; s < g.L; ++s) {
-            host_taps(g.W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride, c->centre_mode);
-            host_taps(g.H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride, c->centre_mode);
+            host_taps(g.W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride, mode);
+            host_taps(g.H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride, mode);
         }
     }
 }
@@ -268,9 +270,14 @@ bool valid_level(const gdp_ctx* c, int b, int o, int s) {
 // C ABI
 // ==========================================================================================
 // Block prefixes of the convolution sweep (kSwWaves strips of conv_rows rows x kSwCols columns)
-// and of the block tiles (conv_block_rows() rows x kSwCols columns).
-static int conv_block_rows(const gdp_ctx* c) { return c->conv_rows != 16 ? c->conv_rows : 16; }
+// and of the block tiles (conv_rows rows x kSwCols columns).
 static int conv_sweep_rows(const gdp_ctx* c) { return c->conv_rows == 32 ? 32 : 16; }
+// The block tiles are instantiated for these (rows per block, waves per block) pairs only: each
+// wave owns whole output rows, so 16 waves take 16/32/48-row tiles and 8 waves 8/16/24/32.
+static bool conv_blk_pair_ok(int rows, int waves) {
+    return waves == 16 ? (rows == 16 || rows == 32 || rows == 48)
+                       : waves == 8 && (rows == 8 || rows == 16 || rows == 24 || rows == 32);
+}
 static void conv_sweep_geom(gdp_ctx* c) {
     Geom& g = c->geom;
     const int strip_cols = SwGeom<kSwV>::kCols;
@@ -283,7 +290,7 @@ static void conv_sweep_geom(gdp_ctx* c) {
         g.sw_strips_c[o] = (og.cols + strip_cols - 1) / strip_cols;
         const long long rows_per_blk = (long long)kSwWaves * conv_sweep_rows(c);
         g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
-        const long long bk_rows = conv_block_rows(c);
+        const long long bk_rows = c->conv_rows;
         g.bk_blk[o + 1] = g.bk_blk[o] + (sweep ? (unsigned)((og.rows + bk_rows - 1) / bk_rows * g.sw_strips_c[o]) : 0u);
         g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
     }
@@ -349,22 +356,27 @@ hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     return hipGetLastError();
 }
 
-// block tiles: (rows per block, waves per block) pairs that are instantiated
+// block tiles: the instantiated (rows per block, waves per block) pairs (conv_blk_pair_ok); the
+// tile grid (bk_blk) was planned for conv_rows, so any other pair is refused, never run with a
+// different tile height
 template <int L>
 hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
-    const int T = conv_block_rows(c), W = c->conv_waves;
-    if (W == 8 || T == 8 || T == 24) { // 8- and 24-row tiles are whole rows per wave only with 8 waves
+    const int T = c->conv_rows, W = c->conv_waves;
+    if (W == 8) {
         switch (T) {
             case 8: return launch_conv_blk_t<L, 8, 8>(c, units, st);
             case 16: return launch_conv_blk_t<L, 16, 8>(c, units, st);
             case 24: return launch_conv_blk_t<L, 24, 8>(c, units, st);
-            default: return launch_conv_blk_t<L, 32, 8>(c, units, st);
+            case 32: return launch_conv_blk_t<L, 32, 8>(c, units, st);
+            default: return hipErrorInvalidConfiguration;
         }
     }
+    if (W != 16) return hipErrorInvalidConfiguration;
     switch (T) {
+        case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
         case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
         case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
-        default: return launch_conv_blk_t<L, 16, 16>(c, units, st);
+        default: return hipErrorInvalidConfiguration;
     }
 }
 
@@ -540,7 +552,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     retile(c, kVariants[c->variant].tile_cols, kVariants[c->variant].tile_rows);
     conv_sweep_geom(c);
     c->h_taps.assign((size_t)tap_off, 0.0f);
-    fill_host_taps(c);
+    fill_host_taps(c, c->centre_mode);
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -574,6 +586,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     if ((e = hipMalloc(&c->d_geom, sizeof(Geom))) != hipSuccess) return hip_fail(e, "hipMalloc(geom)");
     if ((e = hipMalloc(&c->d_taps, std::max<size_t>(4, c->h_taps.size() * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(taps)");
+    c->d_taps_mode[c->centre_mode] = c->d_taps;
     if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)  // int32
         return hip_fail(e, "hipMalloc(input)");
     if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
@@ -606,7 +619,8 @@ void gdp_destroy(gdp_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_geom) (void)hipFree(c->d_geom);
-    if (c->d_taps) (void)hipFree(c->d_taps);
+    for (float* t : c->d_taps_mode)
+        if (t) (void)hipFree(t);
     if (c->d_in_own) (void)hipFree(c->d_in_own);
     for (void* h : c->d_halo_own)
         if (h) (void)hipFree(h);
@@ -826,11 +840,14 @@ int gdp_input_halo(gdp_ctx* c, int side, void** rows, size_t* pitch) try {
         }
         GDP_HIP(c, hipMemset(c->d_halo_own[side], 0, bytes));
     }
+    *rows = c->d_halo_own[side];
+    if (g.halo_ptr[side] == c->d_halo_own[side] && g.halo_rows[side] == n[side] &&
+        g.halo_pitch[side] == c->in_pitch_own)
+        return GDP_OK;  // already bound (every exchange asks again): no geometry upload, no drain
     g.halo_ptr[side] = c->d_halo_own[side];
     g.halo_rows[side] = n[side];
     g.halo_pitch[side] = c->in_pitch_own;
     g.halo_img_stride[side] = (long long)n[side] * c->in_pitch_own;
-    *rows = c->d_halo_own[side];
     return upload_geom(c);
 } GDP_ABI_CATCH(c)
 
@@ -916,10 +933,13 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     // 0) for S = 0..3; both take the octaves whose width is a multiple of 4, the LDS tiles the rest
     // (and everything for other S or conv_kernel = 1)
     const bool sweep = c->conv_kernel != 1 && g.L >= 3 && g.L <= (c->conv_kernel == 2 ? 8 : 6);
-    {  // rows per tile / strip the selected kernel is instantiated for
-        const int r = c->conv_rows, k = c->conv_kernel;
-        const bool ok = k == 0 ? (r == 16 || r == 32) : true;
-        if (sweep && !ok) return c->status(GDP_ERR_STATE, "conv rows %d not available for conv kernel %d", r, k);
+    {  // rows per tile / strip (and waves per block) the selected kernel is instantiated for
+        const int r = c->conv_rows, k = c->conv_kernel, w = c->conv_waves;
+        if (sweep && k == 0 && r != 16 && r != 32)
+            return c->status(GDP_ERR_STATE, "conv rows %d not available for the register sweep (16 or 32)", r);
+        if (sweep && k == 2 && !conv_blk_pair_ok(r, w))
+            return c->status(GDP_ERR_STATE, "conv block tiles: %d rows with %d waves is not an instantiated pair "
+                                            "(16 waves: 16 / 32 / 48 rows; 8 waves: 8 / 16 / 24 / 32 rows)", r, w);
     }
     const unsigned* blk = c->conv_kernel == 2 ? g.bk_blk : g.sw_blk;
     if (sweep && (c->conv_order & 4) && (c->conv_perm_dirty || c->conv_perm_kernel != c->conv_kernel)) {
@@ -1269,10 +1289,22 @@ int gdp_set_window_centre(gdp_ctx* c, int mode) try {
         return c ? c->status(GDP_ERR_ARG, "gdp_set_window_centre: mode must be GDP_CENTRE_SERIAL or GDP_CENTRE_INTLEN") : GDP_ERR_ARG;
     if (mode == c->centre_mode) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
-    GDP_HIP(c, hipDeviceSynchronize());  // no in-flight launch reads a half-written table
+    if (!c->d_taps_mode[mode]) {
+        // first use of this centre: its own table (the other one stays intact for launches already
+        // queued, which captured its pointer), uploaded once; later switches are a pointer swap
+        fill_host_taps(c, mode);
+        float* t = nullptr;
+        hipError_t e = hipMalloc(&t, std::max<size_t>(4, c->h_taps.size() * 4));
+        if (e != hipSuccess) return c->status(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, "hipMalloc(taps)");
+        e = hipMemcpy(t, c->h_taps.data(), c->h_taps.size() * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(t);
+            return c->status(GDP_ERR_HIP, "hipMemcpy(taps): %s", hipGetErrorString(e));
+        }
+        c->d_taps_mode[mode] = t;
+    }
     c->centre_mode = mode;
-    fill_host_taps(c);
-    GDP_HIP(c, hipMemcpy(c->d_taps, c->h_taps.data(), c->h_taps.size() * 4, hipMemcpyHostToDevice));
+    c->d_taps = c->d_taps_mode[mode];
     return GDP_OK;
 } GDP_ABI_CATCH(c)
 

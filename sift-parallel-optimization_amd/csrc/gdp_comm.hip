@@ -269,8 +269,10 @@ int gdp_comm_exchange_halo(gdp_comm* c, gdp_ctx* band, void* stream) try {
     const size_t esz = u8 ? 1 : 4;
     void* halo[2] = {nullptr, nullptr};
     size_t hpitch[2] = {0, 0};
-    for (int side = 0; side < 2; ++side)
-        if (gdp_input_halo(band, side, &halo[side], &hpitch[side]) != GDP_OK) return fail(c, GDP_ERR_NOMEM, gdp_last_error(band));
+    for (int side = 0; side < 2; ++side) {  // binds the band's owned halo rows (a no-op once bound)
+        const int rc = gdp_input_halo(band, side, &halo[side], &hpitch[side]);
+        if (rc != GDP_OK) return fail(c, rc, gdp_last_error(band));
+    }
     int na = 0, nb = 0;
     gdp_conv_halo_rows(band, &na, &nb);
     GDP_HIPC(c, hipSetDevice(c->device));

@@ -20,13 +20,16 @@ Outputs (all plain data, loadable without pickle):
                 mpitest.cpp's GenerateDoG_mpi / GenerateDoG_mpi_omp (:35-189) — run under
                 conda MPICH's mpiexec with S+4 ranks (oracle/_ref/ref_mpi, ref_mpitest)
   checksums_a512omp.json gdp_checksum values of GenerateDoG_nomp_dynamic's output for the bench inputs
+  checksums_inplace.json gdp_checksum values after K in-place calls on the constructor's
+                GaussPyInit — GenerateDoG() K times ("regen", main.cpp:66-73's loop) or GaussFilter
+                of every octave K rounds ("gauss") — for the bench inputs (bench.py --op regen|gauss)
   a512_hashes.json per-level hashes after repeated calls of GaussPyramid_a512omp's
                 GenerateDoG_nomp_dynamic (the AVX-512 x OpenMP subset, :240-364) and GenerateDoG
                 (its DoG-only form, :183-213) — oracle/_ref/ref_avx512 hash-a512omp
   meta.json     generator provenance (glibc, g++, input definitions)
 
 Usage:  make -C oracle ref ref-mpi && python tests/golden/gen_golden.py [--only PART,...]
-        PART: hashes, dumps, taps, checksums, mpi, a512 (default: all)
+        PART: hashes, dumps, taps, checksums, mpi, a512, inplace (default: all)
 """
 import json
 import os
@@ -94,6 +97,10 @@ A512_CASES = [("nomp_dynamic", n, S, inp, calls) for n, S, inp, calls in [
         (3, 2, "lcg:12345", 1), (5, 2, "lcg:12345", 1), (6, 1, "lcg:4", 2), (7, 3, "lcg:12345", 1),
         (64, 2, "lcg:12345", 2), (512, 2, "lcg:12345", 1)]]
 A512_CHECKSUM_CASES = [(4096, 2, "synth:0x5EED:0"), (4096, 2, "synth:0x5EED:1")]
+# in-place re-entry ops after the bench's timed region: (op, calls, n, S, input) — config 2's image
+# and config 4's rank-0 first / last image
+INPLACE_CHECKSUM_CASES = [(op, calls, 4096, 2, f"synth:0x5EED:{i}") for op, calls in (("regen", 3), ("gauss", 2))
+                          for i in (0, 63)]
 TAP_CASES = [(512, 2), (100, 2), (1000, 2), (513, 3), (4096, 2), (1080, 2), (1920, 2), (37, 1)]
 
 
@@ -232,15 +239,43 @@ def gen_a512():
         json.dump(checks, f, indent=1)
 
 
+def gen_inplace():
+    # gdp_checksum after K in-place calls of the serial reference (oracle/_ref/ref_serial regen /
+    # gauss), for bench.py's post-timing parity check of --op regen / --op gauss
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # the checksum formula's numpy restatement (test infrastructure)
+
+    checks = []
+    for op, calls, n, S, inp in INPLACE_CHECKSUM_CASES:
+        pyr = dump(REF_SERIAL, op, n, S, inp, str(calls))
+        sl, _ = level_slices(n, S)
+        acc = 0
+        rec = {"op": op, "calls": calls, "n": n, "S": S, "input": inp,
+               "method": ("GuassDePyramid.h GenerateDoG() x%d" % calls) if op == "regen" else
+                         ("GuassDePyramid.h GaussFilter(o) for every octave, x%d" % calls)}
+        for o in range(octaves_of(n)):
+            m = n >> o
+            for s in range(S + 3):
+                off, _ = sl[(o, s)]
+                acc = (acc + oracle.level_checksum(pyr[off:off + m * m].reshape(m, m), o, s)) & 0xFFFFFFFFFFFFFFFF
+            rec[f"octaves_{o + 1}"] = f"{acc:016x}"
+        checks.append(rec)
+        print("inplace checksum", op, calls, n, inp, flush=True)
+    with open(os.path.join(HERE, "checksums_inplace.json"), "w") as f:
+        json.dump(checks, f, indent=1)
+
+
 def main():
-    parts = {"hashes", "dumps", "taps", "checksums", "mpi", "a512"}
+    parts = {"hashes", "dumps", "taps", "checksums", "mpi", "a512", "inplace"}
     if "--only" in sys.argv:
         parts = set(sys.argv[sys.argv.index("--only") + 1].split(","))
     if "mpi" in parts:
         gen_mpi()
     if "a512" in parts:
         gen_a512()
-    if not parts - {"mpi", "a512"}:
+    if "inplace" in parts:
+        gen_inplace()
+    if not parts - {"mpi", "a512", "inplace"}:
         return
     for b in (REF_SERIAL, REF_AVX512):
         if not os.path.exists(b):

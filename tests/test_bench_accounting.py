@@ -46,20 +46,24 @@ def test_rotation_exceeds_the_infinity_cache():
 
 _RANK_PROBE = r"""
 import json, os, sys, time
-keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "GDP_BENCH_RDV")
 with open(os.path.join(sys.argv[1], "rank%s.json" % os.environ["RANK"]), "w") as f:
     json.dump({"env": {k: os.environ.get(k) for k in keys}, "argv": sys.argv[1:]}, f)
 if len(sys.argv) > 2 and sys.argv[2] == "fail-rank1":
     if os.environ["RANK"] == "1":
+        sys.stderr.write("rank 1 failing on purpose\n")
         sys.exit(3)
     time.sleep(600)  # a rank left waiting in a collective: the launcher must stop it
 """
 
 
-def test_bench_launches_its_own_ranks(tmp_path):
+def test_bench_launches_its_own_ranks(tmp_path, monkeypatch, capfd):
     """`bench.py --gpus N` with no launcher starts N ranks itself: each child
-    gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT and the parent's
-    arguments; a failing rank's status is returned and the other ranks are stopped."""
+    gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1, NO MASTER_PORT (VERDICT r2 item 2:
+    the ranks meet through a file rendezvous in a fresh private directory, GDP_BENCH_RDV, so no
+    port can be taken between its choice and its bind) and the parent's arguments; a failing
+    rank's status is returned, its stderr kept under GDP_BENCH_RANK_LOGS and its tail printed,
+    and the other ranks are stopped."""
     import json
     import time
 
@@ -67,18 +71,68 @@ def test_bench_launches_its_own_ranks(tmp_path):
 
     probe = tmp_path / "probe.py"
     probe.write_text(_RANK_PROBE)
+    logs = tmp_path / "logs"
+    monkeypatch.setenv("GDP_BENCH_RANK_LOGS", str(logs))
+    monkeypatch.setenv("MASTER_PORT", "29500")  # a stale port in the parent's env is not inherited
     assert bench.launch_ranks(3, [str(tmp_path), "ok"], script=str(probe)) == 0
     recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(3)]
-    ports = {r["env"]["MASTER_PORT"] for r in recs}
-    assert len(ports) == 1 and ports.pop().isdigit()
+    rdv = {r["env"]["GDP_BENCH_RDV"] for r in recs}
+    assert len(rdv) == 1
+    rdv = rdv.pop()
+    assert rdv and not os.path.exists(os.path.dirname(rdv))  # private directory, removed afterwards
     for r, rec in enumerate(recs):
         assert rec["env"]["RANK"] == rec["env"]["LOCAL_RANK"] == str(r)
         assert rec["env"]["WORLD_SIZE"] == rec["env"]["LOCAL_WORLD_SIZE"] == "3"
         assert rec["env"]["MASTER_ADDR"] == "127.0.0.1"
+        assert rec["env"]["MASTER_PORT"] is None
         assert rec["argv"] == [str(tmp_path), "ok"]
     t0 = time.time()
+    capfd.readouterr()
     assert bench.launch_ranks(2, [str(tmp_path), "fail-rank1"], script=str(probe)) == 3
     assert time.time() - t0 < 60  # rank 0 (sleeping) was stopped, not waited for
+    assert "rank 1 failing on purpose" in (logs / "rank1.stderr").read_text()
+    err = capfd.readouterr().err
+    assert "rank 1 exited with 3" in err and "rank 1 failing on purpose" in err and str(logs / "rank1.stderr") in err
+
+
+def test_rank_topology_assembly(monkeypatch):
+    """The N-rank line certifies itself: rank_topology gathers every rank's
+    device identity and counts the ranks with an all_reduce of ones.  A gloo rehearsal with two
+    ranks on one device says so explicitly; under nccl the same shared device is fatal."""
+    import types
+
+    import bench
+
+    class FakeDist:
+        def __init__(self, devs, count):
+            self.devs, self.count = devs, count
+
+        def all_gather_object(self, out, obj):
+            out[:] = self.devs
+
+        def all_reduce(self, t):
+            t.fill_(self.count)
+
+    props = types.SimpleNamespace(name="AMD Instinct MI355X", pci_domain_id=0, pci_bus_id=0x75, pci_device_id=0,
+                                  uuid="GPU-aa")
+    import torch
+
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props)
+    args = types.SimpleNamespace(gpus=2)
+    same = [{"rank": r, "device": 0, "pci": "0000:75:00.0", "uuid": "GPU-aa"} for r in range(2)]
+    topo = bench.rank_topology(2, 0, 0, "gloo", FakeDist(same, 2), args)
+    assert topo["backend"] == "gloo" and topo["collective_world"] == 2 and topo["distinct_devices"] == 1
+    assert "rccl_world" not in topo and "not a multi-GPU measurement" in topo["note"]
+    monkeypatch.setattr(torch, "ones", lambda *a, **k: torch.zeros(1, dtype=torch.int64))  # no GPU here
+    with pytest.raises(SystemExit, match="distinct devices"):
+        bench.rank_topology(2, 0, 0, "nccl", FakeDist(same, 2), args)
+    two = [dict(same[0]), dict(same[1], device=1, pci="0000:05:00.0", uuid="GPU-bb")]
+    topo = bench.rank_topology(2, 0, 0, "nccl", FakeDist(two, 2), args)
+    assert topo["rccl_world"] == 2 and topo["distinct_devices"] == 2 and topo["backend"] == "rccl"
+    with pytest.raises(SystemExit, match="RCCL counted 1 ranks"):
+        bench.rank_topology(2, 0, 0, "nccl", FakeDist(two, 1), args)
+    one = bench.rank_topology(1, 0, 0, "nccl", None, types.SimpleNamespace(gpus=1))
+    assert one["collective_world"] == 1 and one["devices"][0]["pci"] == "0000:75:00.0"
 
 
 def _run_bench(env_extra, *args):

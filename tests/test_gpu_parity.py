@@ -386,6 +386,21 @@ def test_errors_are_loud(pkg):
         pkg.PyramidContext(32, 32, S=2, octaves=9)
 
 
+def test_conv_block_tiles_refuse_uninstantiated_pairs(pkg):
+    """the block tiles' grid is planned for conv_rows, so a (rows, waves) pair with no
+    kernel instance (48 rows on 8 waves, 8 rows on 16) is refused with an error — never run with
+    a kernel of another tile height that would leave rows unwritten and still return ok."""
+    with pkg.PyramidContext(256, 256, S=2, octaves=3) as ctx:
+        ctx.fill_synthetic(7, 0)
+        for rows, waves in ((48, 8), (8, 16), (24, 16)):
+            ctx.set_tuning(conv_kernel=2, conv_rows=rows, conv_waves=waves)
+            with pytest.raises(pkg.GdpError, match="not an instantiated pair"):
+                ctx.build_gaussian()
+        ctx.set_tuning(conv_rows=48, conv_waves=16)
+        ctx.build_gaussian()
+        ctx.sync()
+
+
 # ------------------------------------------------------------------ full-size properties
 def test_config3_batch_1080p(pkg, oracle):
     """64 x 1080x1920, 5 octaves (BASELINE config 3) — a spread of images checked exactly."""
@@ -622,6 +637,43 @@ def _assert_hashes(oracle, pyr, rec, what):
             assert oracle.fnv(lv[(o, s)]) == int(h, 16), (what, n, S, rec["input"], o, s)
 
 
+def test_cpp_single_gpu_generate_dog_mpi_matches_the_mpi_variant(oracle, tmp_path):
+    """GaussPyramid_hip::GenerateDoG_mpi — the exact call main.cpp:68 makes — reproduces
+    GaussPyramid_mpi::GenerateDoG_mpi's collector (GaussDePyramid-MPI.h:265-335, run under mpiexec
+    with S+4 ranks: tests/golden/mpi_hashes.json) for EVERY n, including n = 100 / 1000 / 96 where
+    its integer-length window centre (:273) differs from the serial header's; and the context
+    returns to the serial centre, so a later GenerateDoG() is GuassDePyramid.h's."""
+    exe = os.path.join(REPO, "examples", "main_hip")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
+    out = tmp_path / "s.f32"
+    recs = _mpi_records("GaussDePyramid-MPI.h:GenerateDoG_mpi")
+    assert {r["n"] for r in recs} >= {100, 1000, 96, 512} and any(not r["equals_serial"] for r in recs)
+    for rec in recs:
+        n, S, spec = rec["n"], rec["S"], rec["input"]
+        subprocess.run([exe, str(n), str(S), spec, str(out), "1", "mpi"], check=True, timeout=120)
+        got = np.fromfile(out, dtype=np.float32)
+        _assert_hashes(oracle, got, rec, "GaussPyramid_hip::GenerateDoG_mpi")
+        if not rec["equals_serial"]:
+            assert not np.array_equal(_bits(got), _bits(oracle.build_pyramid(oracle.image_from_spec(n, spec), S)))
+    # re-entry (main.cpp:66-73 calls it back to back) and the centre restored for GenerateDoG()
+    n, S, spec = 100, 2, "lcg:5"
+    img = oracle.image_from_spec(n, spec)
+    O = oracle.octaves(n)
+    for calls in (2, 3):
+        subprocess.run([exe, str(n), str(S), spec, str(out), str(calls), "mpi"], check=True, timeout=120)
+        want = oracle.init_pyramid(img, S)
+        for _ in range(calls):
+            oracle.generate_dog(want, n, n, S, O, centre="intlen")
+        _assert_same(np.fromfile(out, dtype=np.float32), want, ("GenerateDoG_mpi re-entry", calls))
+    for calls in (2, 3):  # GenerateDoG_mpi, GenerateDoG, GenerateDoG_mpi: each call keeps its own centre
+        subprocess.run([exe, str(n), str(S), spec, str(out), str(calls), "mixed"], check=True, timeout=120)
+        want = oracle.init_pyramid(img, S)
+        for c in range(calls):
+            oracle.generate_dog(want, n, n, S, O, centre="intlen" if c % 2 == 0 else "serial")
+        _assert_same(np.fromfile(out, dtype=np.float32), want, ("GenerateDoG_mpi / GenerateDoG mixed", calls))
+
+
 def test_cpp_mpitest_dropin_matches_the_reference_mpitest(oracle, tmp_path):
     """mpitest.cpp's free-function API (GaussPyInit(int**), GenerateDoG_mpi / _mpi_omp, delete_mpi)
     on the GPU == the collector's pyramid of mpitest.cpp ITSELF run under mpiexec with S+4 ranks
@@ -796,7 +848,7 @@ _CONV_KERNELS = [dict(conv_kernel=0, conv_rows=16, conv_order=0), dict(conv_kern
                  dict(conv_kernel=0, conv_rows=16, conv_order=3), dict(conv_kernel=0, conv_rows=32, conv_order=2),
                  dict(conv_kernel=0, conv_rows=16, conv_order=4), dict(conv_kernel=0, conv_rows=32, conv_order=5),
                  dict(conv_kernel=1), dict(conv_kernel=2, conv_rows=16, conv_order=0),
-                 dict(conv_kernel=2, conv_rows=8, conv_order=5), dict(conv_kernel=2, conv_rows=32, conv_order=4),
+                 dict(conv_kernel=2, conv_rows=8, conv_waves=8, conv_order=5), dict(conv_kernel=2, conv_rows=32, conv_order=4),
                  dict(conv_kernel=2, conv_rows=48, conv_order=1), dict(conv_kernel=2, conv_rows=24, conv_waves=8, conv_order=4),
                  dict(conv_kernel=2, conv_rows=32, conv_waves=8, conv_order=1)]
 
@@ -1031,20 +1083,28 @@ def _rank_failure(stderr):
     return "\n".join(lines[tb[0]:] if tb else lines)[-6000:]
 
 
-def test_bench_selflaunched_ranks_certify_their_work():
+def test_bench_selflaunched_ranks_certify_their_work(tmp_path):
     """bench.py --gpus 2 started without a launcher (the driver's command form) on this one GPU,
     ranks over gloo: the default build certifies both ranks' images bit-exact, and the banded
-    convolution (config 5) exchanges halo rows every step and certifies bands == whole image."""
+    convolution (config 5) exchanges halo rows every step and certifies bands == whole image.
+    The ranks meet through launch_ranks' file rendezvous (no port), each rank's stderr is kept
+    under the test's tmp path (named in a failure), and the line's topology block records both
+    ranks on the ONE shared device (a rehearsal, not a 2-GPU measurement)."""
     import json
 
-    env = dict(os.environ, GDP_BENCH_BACKEND="gloo")
     for args, key in ((["--steps", "5", "--warmup", "1", "--no-cpu", "--no-autotune"], "build"),
                       (["--op", "conv", "--config", "c5", "--steps", "2", "--warmup", "1"], "conv")):
+        logs = tmp_path / key
+        env = dict(os.environ, GDP_BENCH_BACKEND="gloo", GDP_BENCH_RANK_LOGS=str(logs))
         r = subprocess.run(["python3", os.path.join(REPO, "bench.py"), "--gpus", "2"] + args, env=env, timeout=240,
                            capture_output=True, text=True)
-        assert r.returncode == 0, (key, _rank_failure(r.stderr))
+        assert r.returncode == 0, (key, f"rank stderr kept in {logs}", _rank_failure(r.stderr))
         line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
         assert line["n_gpus"] == 2, key
+        topo = line["topology"]
+        assert topo["backend"] == "gloo" and topo["collective_world"] == 2 and topo["distinct_devices"] == 1, topo
+        assert [d["rank"] for d in topo["devices"]] == [0, 1] and "not a multi-GPU measurement" in topo["note"]
+        assert [p["rank"] for p in topo["per_rank"]] == [0, 1] and all(p["kernel_ms"] > 0 for p in topo["per_rank"])
         if key == "build":
             assert line["parity"]["status"] == "bit-exact" and line["parity"]["ranks_certified"] == [0, 1]
         else:

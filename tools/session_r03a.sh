@@ -1,0 +1,7 @@
+# round-3 session a: the GPU suite (GenerateDoG_mpi centre fix, refused conv pairs, topology /
+# file-rendezvous self-launch), the default bench line, and the in-place lines with their new parity
+exec tools/gpu_session.sh \
+  "gputest_r03a|600|python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider" \
+  "bench_c2_r03a|300|python3 bench.py" \
+  "bench_regen_c2_r03a|200|python3 bench.py --op regen --no-cpu" \
+  "bench_gauss_c2_r03a|200|python3 bench.py --op gauss --no-cpu"
