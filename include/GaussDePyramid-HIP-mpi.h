@@ -14,8 +14,13 @@
 // (:265-335); the collector's GaussPy ends as the full pyramid.  Here ANY number of ranks works:
 // rank r builds row band gdp_band_rows(n, size, r, layer) of every level on GPU r % devices,
 // and rank 0 — the collector — receives every band into its whole-image context and mirrors it
-// into GaussPy; other ranks' GaussPy keep their contents (the reference's workers also end with
-// partial data).  The collector's pyramid is bit-identical to the reference's collector for EVERY
+// into GaussPy.  Worker state differs from the reference's, by design: there rank i < S+3 ends
+// holding scale i of every octave windowed (the other scales keep their GaussPyInit values, :271-291),
+// rank S+3 is the collector and ranks > S+3 are untouched; here the collector is rank 0 and every
+// other rank's GaussPy keeps what it held before the call (its band's rows live only in its device
+// band context).  No caller in the reference reads a worker's GaussPy (main.cpp:61-74 only times
+// the call), and the reference's role map needs >= S+4 ranks where this one takes any number.
+// The collector's pyramid is bit-identical to the reference's collector for EVERY
 // n: GenerateDoG_mpi centres its windows on the integer octave length (`l = float(len-1)/2`,
 // :273 — GDP_CENTRE_INTLEN), while GaussFilter/GenerateDoG use the float-halved centre of
 // :134-143 like GuassDePyramid.h (the two differ only when n is not a multiple of 2^(layer-1),

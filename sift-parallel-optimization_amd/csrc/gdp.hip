@@ -273,9 +273,10 @@ bool valid_level(const gdp_ctx* c, int b, int o, int s) {
 // and of the block tiles (conv_rows rows x kSwCols columns).
 static int conv_sweep_rows(const gdp_ctx* c) { return c->conv_rows == 32 ? 32 : 16; }
 // The block tiles are instantiated for these (rows per block, waves per block) pairs only: each
-// wave owns whole output rows, so 16 waves take 16/32/48-row tiles and 8 waves 8/16/24/32.
+// wave owns whole output rows, so 16 waves take 16/32/48/64-row tiles and 8 waves 8/16/24/32
+// (64 rows: 80 staged rows = 80 KB of LDS, two blocks per CU).
 static bool conv_blk_pair_ok(int rows, int waves) {
-    return waves == 16 ? (rows == 16 || rows == 32 || rows == 48)
+    return waves == 16 ? (rows == 16 || rows == 32 || rows == 48 || rows == 64)
                        : waves == 8 && (rows == 8 || rows == 16 || rows == 24 || rows == 32);
 }
 static void conv_sweep_geom(gdp_ctx* c) {
@@ -376,6 +377,7 @@ hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
         case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
         case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
         case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
+        case 64: return launch_conv_blk_t<L, 64, 16>(c, units, st);
         default: return hipErrorInvalidConfiguration;
     }
 }
@@ -939,7 +941,7 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
             return c->status(GDP_ERR_STATE, "conv rows %d not available for the register sweep (16 or 32)", r);
         if (sweep && k == 2 && !conv_blk_pair_ok(r, w))
             return c->status(GDP_ERR_STATE, "conv block tiles: %d rows with %d waves is not an instantiated pair "
-                                            "(16 waves: 16 / 32 / 48 rows; 8 waves: 8 / 16 / 24 / 32 rows)", r, w);
+                                            "(16 waves: 16 / 32 / 48 / 64 rows; 8 waves: 8 / 16 / 24 / 32 rows)", r, w);
     }
     const unsigned* blk = c->conv_kernel == 2 ? g.bk_blk : g.sw_blk;
     if (sweep && (c->conv_order & 4) && (c->conv_perm_dirty || c->conv_perm_kernel != c->conv_kernel)) {
@@ -1424,9 +1426,9 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             c->conv_kernel = value;
             return GDP_OK;
         case GDP_TUNE_CONV_ROWS: {
-            if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48)
-                return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32 or 48 (sweep: 16 / 32; block tiles: "
-                                              "16 / 32 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8)");
+            if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48 && value != 64)
+                return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32, 48 or 64 (sweep: 16 / 32; block "
+                                              "tiles: 16 / 32 / 48 / 64 with 16 waves, 8 / 16 / 24 / 32 with 8)");
             const int old = c->conv_rows;
             c->conv_rows = value;
             conv_sweep_geom(c);

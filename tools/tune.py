@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
     ap.add_argument("--S", type=int, default=2, help="scales parameter S (S + 3 levels per octave)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
+    ap.add_argument("--checksums", action="store_true",
+                    help="print gdp_checksum of image 0 after each variant's warm-up build (A/B of library builds: "
+                         "compare across GDP_LIBRARY runs)")
     ap.add_argument("--rotate", type=int, default=1,
                     help="buffer sets the timed launches cycle through (bench.py's cold-cache steps)")
     args = ap.parse_args()
@@ -71,6 +74,8 @@ def main():
         apply(kw)
         {"conv": ctx.build_gaussian, "subset": ctx.build_subset}.get(kw["op"], ctx.build)()
         ctx.sync()
+        if args.checksums:
+            print(json.dumps({"variant": name, "shape": [H, W, B], "checksum0": f"{ctx.checksum(0):016x}"}), flush=True)
         lev = ctx.level(0, 0, 0)
         ref = refs.setdefault(kw["op"], lev)
         if args.no_check:
