@@ -253,9 +253,15 @@ void fill_host_taps(gdp_ctx* c, int mode) {
     const Geom& g = c->geom;
     for (int o = 0; o < g.O; ++o) {
         const OctGeom& og = g.oct[o];
+        std::vector<float> rows(og.rtap_row == 1 ? 0 : (size_t)(g.H >> o));
         for (int s = 0; s < g.L; ++s) {
             host_taps(g.W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride, mode);
-            host_taps(g.H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride, mode);
+            if (og.rtap_row == 1) {  // contiguous per scale (a square image's: the column taps again)
+                host_taps(g.H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride, mode);
+                continue;
+            }
+            const int n = host_taps(g.H, o, s, rows.data(), mode);  // [row][scale] interleaved
+            for (int r = 0; r < n; ++r) c->h_taps[og.rtap + (size_t)r * og.rtap_row + s] = rows[r];
         }
     }
 }
@@ -499,6 +505,9 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // optional padding between levels (floats, multiple of 64) — layout experiment knob
     const char* pad_env = std::getenv("GDP_LEVEL_PAD");
     const long long level_pad = pad_env ? round_up(std::max(0ll, std::atoll(pad_env)), kLevelAlign) : 0;
+    // row-window layout of a non-square image (GDP_ROWTAP_LAYOUT: 0 [scale][row], 1 [row][scale])
+    const char* rl_env = std::getenv("GDP_ROWTAP_LAYOUT");
+    const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : false;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
     long long tap_off = 0, lev_off = 0, grp = 0;
     for (int o = 0; o < O; ++o) {
@@ -522,11 +531,20 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         // 1.28 ms).  Bit-identical either way.
         if (H == W) {
             og.rtap_stride = og.ctap_stride;
+            og.rtap_row = 1;
             og.rtap = og.ctap;
-        } else {
+        } else if (!rowtap_interleave) {
             og.rtap_stride = (int)round_up(Hg, 4);
+            og.rtap_row = 1;
             og.rtap = (int)tap_off;
             tap_off += (long long)og.rtap_stride * g.L;
+        } else {
+            // [row][scale]: the S+3 windows of a row are adjacent, so a tile's rows of one octave
+            // touch ~L/32 lines per row instead of one line per scale
+            og.rtap_stride = 1;
+            og.rtap_row = g.L;
+            og.rtap = (int)tap_off;
+            tap_off += round_up((long long)Hg * g.L, 4);
         }
         og.grp_begin = grp;
         make_magic((unsigned)std::max(1, og.gpr), &og.gpr_magic, &og.gpr_shift);
@@ -1219,7 +1237,13 @@ int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) try {
     const int n = axis == 0 ? og.cols : (c->geom.H >> o);
     const long long off = axis == 0 ? og.ctap + (long long)s * og.ctap_stride : og.rtap + (long long)s * og.rtap_stride;
     // read back what the device holds, not the host copy: this is what the kernels use
-    GDP_HIP(c, hipMemcpy(host, c->d_taps + off, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (axis == 0 || og.rtap_row == 1) {
+        GDP_HIP(c, hipMemcpy(host, c->d_taps + off, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return GDP_OK;
+    }
+    std::vector<float> rows((size_t)n * og.rtap_row);  // [row][scale]: pick scale s of each row
+    if (n > 0) GDP_HIP(c, hipMemcpy(rows.data(), c->d_taps + og.rtap, rows.size() * 4, hipMemcpyDeviceToHost));
+    for (int r = 0; r < n; ++r) host[r] = rows[(size_t)r * og.rtap_row + s];
     return GDP_OK;
 } GDP_ABI_CATCH(c)
 

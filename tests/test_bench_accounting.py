@@ -190,3 +190,20 @@ def test_subset_traffic_records_name_their_template_instance():
     full = bench.latest_pmc("c2", 15, 0, "build", 5)
     assert full is not None and full["file"] != rec["file"]
     assert bench.latest_pmc("c2", 15, 0, "subset", 4) is None  # no k_build<0, ...> subset record
+
+
+def test_inplace_traffic_records_name_their_block_shape():
+    """bench.py --op regen / --op gauss attach PMC traffic only from a record of the same in-place
+    kernel instance: every block shape the autotune can pick on config 2 has one,
+    keyed by GDP_TUNE_INPLACE_SUB / _WINDOW_SUB, naming its template instance."""
+    import bench
+
+    for op, key, subs, kern in (("regen", "inplace_sub", (1, 4, 2, 0), "k_levels"), ("gauss", "window_sub", (1, 4, 2), "k_window")):
+        for sub in subs:
+            rec = bench.latest_inplace_pmc("c2", op, {key: sub})
+            assert rec is not None and rec["op"] == op and rec[key] == sub, (op, sub)
+            assert kern in rec["kernel"] and ("k_levels_x" in rec["kernel"]) == (op == "regen" and sub == 0)
+            assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
+            assert rec["bench_line_of_traced_run"]["parity"]["status"] == "bit-exact"
+    assert bench.latest_inplace_pmc("c2", "regen", {"inplace_sub": 3}) is None
+    assert bench.latest_inplace_pmc("c4", "gauss", {"window_sub": 4}) is None

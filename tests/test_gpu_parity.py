@@ -857,7 +857,8 @@ _CONV_KERNELS = [dict(conv_kernel=0, conv_rows=16, conv_order=0), dict(conv_kern
 @pytest.mark.parametrize("H,W,S,O,fmt,batch", _CONV_SHAPES)
 @pytest.mark.parametrize("tune", _CONV_KERNELS, ids=["sweep16", "sweep32", "sweep16xcd_alt", "sweep32alt",
                                                           "sweep16rowmix", "sweep32rowmix_xcd", "tiles", "blk16",
-                                                          "blk8rowmix_xcd", "blk32rowmix", "blk48xcd", "blk24w8rowmix", "blk32w8xcd"])
+                                                          "blk8rowmix_xcd", "blk32rowmix", "blk48xcd", "blk24w8rowmix", "blk32w8xcd",
+                                                          "blk64rowmix", "blk64xcd"])
 def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt, batch, tune):
     """Extension mode (no reference counterpart; parity unpinned by construction): checked against
     a float64 separable convolution, for both kernels (register sweep with DPP lane shifts, LDS
