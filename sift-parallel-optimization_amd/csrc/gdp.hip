@@ -279,10 +279,13 @@ bool valid_level(const gdp_ctx* c, int b, int o, int s) {
 // and of the block tiles (conv_rows rows x kSwCols columns).
 static int conv_sweep_rows(const gdp_ctx* c) { return c->conv_rows == 32 ? 32 : 16; }
 // The block tiles are instantiated for these (rows per block, waves per block) pairs only: each
-// wave owns whole output rows, so 16 waves take 16/32/48/64-row tiles and 8 waves 8/16/24/32
-// (64 rows: 80 staged rows = 80 KB of LDS, two blocks per CU).
+// wave owns whole output rows, so 16 waves take 16/32/48-row tiles and 8 waves 8/16/24/32.
+// (Measured and dropped, round 3: 64-row tiles on 16 waves — 80 staged rows, 80 KB of LDS, two
+// blocks per CU — cut the staged-row overhead from 44/32 to 76/64 but ran slower on every config:
+// 4096^2 0.110 vs 0.099 ms, 64 x 1080 x 1920 0.767 vs 0.714, 64 x 4096^2 5.95 vs 5.71, 16384^2
+// 1.48 vs 1.45; profiles/conv_ab_r03c.log.)
 static bool conv_blk_pair_ok(int rows, int waves) {
-    return waves == 16 ? (rows == 16 || rows == 32 || rows == 48 || rows == 64)
+    return waves == 16 ? (rows == 16 || rows == 32 || rows == 48)
                        : waves == 8 && (rows == 8 || rows == 16 || rows == 24 || rows == 32);
 }
 static void conv_sweep_geom(gdp_ctx* c) {
@@ -383,7 +386,6 @@ hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
         case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
         case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
         case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
-        case 64: return launch_conv_blk_t<L, 64, 16>(c, units, st);
         default: return hipErrorInvalidConfiguration;
     }
 }
@@ -505,9 +507,13 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // optional padding between levels (floats, multiple of 64) — layout experiment knob
     const char* pad_env = std::getenv("GDP_LEVEL_PAD");
     const long long level_pad = pad_env ? round_up(std::max(0ll, std::atoll(pad_env)), kLevelAlign) : 0;
-    // row-window layout of a non-square image (GDP_ROWTAP_LAYOUT: 0 [scale][row], 1 [row][scale])
+    // Row-window layout of a non-square image: [row][scale] (default) or, with GDP_ROWTAP_LAYOUT=0,
+    // [scale][row].  A tile's rows then read their S+3 windows from ~L/32 lines per row instead of
+    // one cold line per scale: 65536 x 4096 builds in 1.227 vs 1.43-1.46 ms (v15), 16384 x 4096 in
+    // 0.315 vs 0.363 ms — the speed of row windows that are always hot (timing-only build, 1.25
+    // ms); config 3 and the in-place passes unchanged (profiles/ab_rowtap_r03c.log, bit-exact)
     const char* rl_env = std::getenv("GDP_ROWTAP_LAYOUT");
-    const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : false;
+    const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : true;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
     long long tap_off = 0, lev_off = 0, grp = 0;
     for (int o = 0; o < O; ++o) {
@@ -959,7 +965,7 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
             return c->status(GDP_ERR_STATE, "conv rows %d not available for the register sweep (16 or 32)", r);
         if (sweep && k == 2 && !conv_blk_pair_ok(r, w))
             return c->status(GDP_ERR_STATE, "conv block tiles: %d rows with %d waves is not an instantiated pair "
-                                            "(16 waves: 16 / 32 / 48 / 64 rows; 8 waves: 8 / 16 / 24 / 32 rows)", r, w);
+                                            "(16 waves: 16 / 32 / 48 rows; 8 waves: 8 / 16 / 24 / 32 rows)", r, w);
     }
     const unsigned* blk = c->conv_kernel == 2 ? g.bk_blk : g.sw_blk;
     if (sweep && (c->conv_order & 4) && (c->conv_perm_dirty || c->conv_perm_kernel != c->conv_kernel)) {
@@ -1450,9 +1456,9 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             c->conv_kernel = value;
             return GDP_OK;
         case GDP_TUNE_CONV_ROWS: {
-            if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48 && value != 64)
-                return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32, 48 or 64 (sweep: 16 / 32; block "
-                                              "tiles: 16 / 32 / 48 / 64 with 16 waves, 8 / 16 / 24 / 32 with 8)");
+            if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48)
+                return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32 or 48 (sweep: 16 / 32; block tiles: "
+                                              "16 / 32 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8)");
             const int old = c->conv_rows;
             c->conv_rows = value;
             conv_sweep_geom(c);

@@ -256,7 +256,7 @@ class PyramidContext:
         """Performance knobs of the kernels (outputs are bit-identical for every setting; the
         conv_* knobs select the convolution extension's kernel: 0 register sweep, 1 LDS tiles,
         2 block tiles, and the sweep's rows per wave strip (16 / 32) or the block tiles' rows per
-        block with conv_waves waves per block (16 waves: 16 / 32 / 48 / 64 rows; 8 waves: 8 / 16 / 24 /
+        block with conv_waves waves per block (16 waves: 16 / 32 / 48 rows; 8 waves: 8 / 16 / 24 /
         32 rows — any other pair makes build_gaussian raise GdpError); stage_kb / stage_threads
         size the double-buffered pinned staging of the row-pointer downloads)."""
         vals = dict(nontemporal=nontemporal, blocks_per_cu=blocks_per_cu, grid=grid, variant=variant,

@@ -156,8 +156,7 @@ N_CONV_CASES = 120
 _CONV_TUNES = [dict(conv_kernel=2, conv_rows=32, conv_order=4), dict(conv_kernel=2, conv_rows=16, conv_order=0),
                dict(conv_kernel=2, conv_rows=48, conv_order=5), dict(conv_kernel=2, conv_rows=24, conv_waves=8, conv_order=1),
                dict(conv_kernel=2, conv_rows=8, conv_waves=8, conv_order=4), dict(conv_kernel=0, conv_rows=16, conv_order=5),
-               dict(conv_kernel=0, conv_rows=32, conv_order=2), dict(conv_kernel=1),
-               dict(conv_kernel=2, conv_rows=64, conv_order=4)]
+               dict(conv_kernel=0, conv_rows=32, conv_order=2), dict(conv_kernel=1)]
 
 
 def _conv_ref(pkg, img, S, O):
