@@ -714,10 +714,9 @@ def main():
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
-    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4, 8],
+    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4],
                     help="--op regen/gauss: force the in-place block shape (GDP_TUNE_INPLACE_SUB / _WINDOW_SUB: "
-                         "1024 / N threads, 0 = k_levels_x, 8 = k_levels_w) and skip its autotune, e.g. for "
-                         "profiling runs")
+                         "1024 / N threads, 0 = k_levels_x) and skip its autotune, e.g. for profiling runs")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
                     help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv", "subset"],
@@ -879,7 +878,7 @@ def main():
             c.build(stream)  # materialise the pyramid the in-place passes work on
         steps_fn = [c.generate_dog if args.op == "regen" else (lambda st, c=c: c.gauss_range(0, O, st))
                     for c in ctxs]
-        key, values = ("inplace_sub", [1, 4, 2, 0, 8]) if args.op == "regen" else ("window_sub", [1, 4, 2])
+        key, values = ("inplace_sub", [1, 4, 2, 0]) if args.op == "regen" else ("window_sub", [1, 4, 2])
         if args.inplace_sub is not None:
             if args.inplace_sub not in values:
                 sys.exit(f"bench.py: --inplace-sub {args.inplace_sub} is not a {key} value ({values})")
@@ -996,8 +995,6 @@ def main():
                        "variant %d, tile order %d" % (ctx.tuning()["variant"], ctx.tuning()["tile_order"])
                        if args.op == "subset" else
                        {"regen": ("k_levels_x (in-place window+DoG, one level per wave)" if tun["inplace_sub"] == 0 else
-                                  "k_levels_w (in-place window+DoG, the levels of 12 groups across one wave's lanes, "
-                                  "no barrier)" if tun["inplace_sub"] == 8 else
                                   "k_levels<MODE=3> (in-place window+DoG, all octaves, %d-thread blocks)"
                                   % (1024 // tun["inplace_sub"])) + (" (autotuned)" if autotuned else ""),
                         "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks)%s"

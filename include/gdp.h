@@ -271,8 +271,7 @@ enum {
                                    2 XCD row-interleaved                                       */
     GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk
                                    (default 4 up to 32 Mpix per launch, else 1; or 2);
-                                   0 = one level per wave (k_levels_x); 8 = the levels of a
-                                   group across one wave's lanes, no barrier (k_levels_w) */
+                                   0 = one level per wave (k_levels_x) */
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (S <= 3), 1 LDS tiles,
                                    2 block tiles (default; one output row per wave, S <= 5) */

@@ -231,17 +231,6 @@ int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st) {
 template <int MODE>
 int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     const Geom& g = c->geom;
-    if ((MODE == 2 || MODE == 3) && c->inplace_sub == 8) {  // k_levels_w: levels across one wave's lanes
-        constexpr int kWpb = 4;
-        const long long waves = ((long long)g.lw_blk[oe] - g.lw_blk[ob]) * g.batch;
-        if (waves <= 0) return GDP_OK;
-        const long long grid = (waves + kWpb - 1) / kWpb;
-        if (grid >= (1ll << 31) || waves >= (1ll << 32)) return c->status(GDP_ERR_ARG, "in-place pass too large for one launch");
-        auto kern = c->nontemporal ? k_levels_w<MODE == 3 ? 3 : 2, true, kWpb> : k_levels_w<MODE == 3 ? 3 : 2, false, kWpb>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * kWpb), 0, st, c->d_geom, c->d_out, c->d_taps, ob, oe);
-        GDP_HIP(c, hipGetLastError());
-        return GDP_OK;
-    }
     if ((MODE == 2 || MODE == 3) && c->inplace_sub == 0 && g.L <= 16) {
         const long long grid = ((long long)g.lx_blk[oe] - g.lx_blk[ob]) * g.batch;
         if (grid <= 0) return GDP_OK;
@@ -510,8 +499,6 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     g.in_row0 = row_begin;
     g.in_rows = row_end - row_begin;
     g.in_pitch = round_up(W, 4);
-    g.lw_g = std::max(1, 64 / g.L);
-    if (g.lw_g >= 4) g.lw_g &= ~3;  // lane quads stay within one level (64 contiguous bytes)
     g.in_img_stride = (long long)g.in_rows * g.in_pitch;
     g.vec_in = 1;
     c->in_pitch_own = g.in_pitch;
@@ -570,7 +557,6 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         grp += (long long)og.rows * og.gpr;
         g.lv_blk[o + 1] = g.lv_blk[o] + (unsigned)(((long long)og.rows * og.gpr + kLevBlock - 1) / kLevBlock);
         g.lx_blk[o + 1] = g.lx_blk[o] + (unsigned)(((long long)og.rows * og.gpr + 63) / 64);
-        g.lw_blk[o + 1] = g.lw_blk[o] + (unsigned)(((long long)og.rows * og.gpr + g.lw_g - 1) / g.lw_g);
         g.cv_tiles_c[o] = (og.cols + kCvTW - 1) / kCvTW;
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
@@ -1460,9 +1446,8 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             return GDP_OK;
         case GDP_TUNE_INPLACE_SUB:
         case GDP_TUNE_WINDOW_SUB:
-            if ((value != 1 && value != 2 && value != 4) && !(key == GDP_TUNE_INPLACE_SUB && (value == 0 || value == 8)))
-                return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4 (in-place DoG also 0: one level per wave, "
-                                              "8: the levels across one wave's lanes)");
+            if ((value != 1 && value != 2 && value != 4) && !(key == GDP_TUNE_INPLACE_SUB && value == 0))
+                return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4 (in-place DoG also 0: one level per wave)");
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
         case GDP_TUNE_CONV_KERNEL:

@@ -329,7 +329,7 @@ def test_int_star_star_upload(pkg, oracle):
 
 
 # ------------------------------------------------------------------ in-place ops / re-entry
-@pytest.mark.parametrize("sub", [0, 1, 8])
+@pytest.mark.parametrize("sub", [0, 1])
 def test_inplace_ops_match_reference_order(pkg, oracle, sub):
     H, W, S = 72, 104, 2
     O = oracle.default_octaves(H, W)
@@ -352,12 +352,11 @@ def test_inplace_ops_match_reference_order(pkg, oracle, sub):
         _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
 
 
-@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0), (1, 8), (0, 8)])
+@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0)])
 def test_gauss_range_and_store_modes(pkg, oracle, nt, sub):
     """One-launch GaussFilter over an octave range == per-octave GaussFilter; both store modes;
     every in-place DoG kernel (sub 0 = one level per wave, k_levels_x; S = 14 has 17 levels and
-    falls back to k_levels; sub 8 = the levels across one wave's lanes, k_levels_w: 12 groups per
-    wave at S = 2, 20 at S = 0, 8 at S = 4, 3 at S = 14); a batch of 3 and generic-S contexts."""
+    falls back to k_levels); a batch of 3 and generic-S contexts."""
     for H, W, S, B in [(90, 200, 2, 3), (64, 48, 4, 1), (40, 36, 14, 1), (52, 66, 0, 2)]:
         O = oracle.default_octaves(H, W)
         imgs = [oracle.lcg_image(H, W, 5 + b) for b in range(B)]
