@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
     ap.add_argument("--S", type=int, default=2, help="scales parameter S (S + 3 levels per octave)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
+    ap.add_argument("--octaves", type=int, default=None, help="octave count overriding the config's")
     ap.add_argument("--checksums", action="store_true",
                     help="print gdp_checksum of image 0 after each variant's warm-up build (A/B of library builds: "
                          "compare across GDP_LIBRARY runs)")
@@ -43,6 +44,8 @@ def main():
     H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
     if args.shape:
         H, W, B = (int(x) for x in args.shape.split("x"))
+    if args.octaves:
+        O = args.octaves
     ctxs = [pkg.PyramidContext(H, W, S=args.S, octaves=O, batch=B) for _ in range(args.rotate)]
     for c in ctxs:
         c.fill_synthetic(bench.SEED, 0)
