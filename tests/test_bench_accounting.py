@@ -195,15 +195,40 @@ def test_subset_traffic_records_name_their_template_instance():
 def test_inplace_traffic_records_name_their_block_shape():
     """bench.py --op regen / --op gauss attach PMC traffic only from a record of the same in-place
     kernel instance: every block shape the autotune can pick on config 2 has one,
-    keyed by GDP_TUNE_INPLACE_SUB / _WINDOW_SUB, naming its template instance."""
+    keyed by GDP_TUNE_INPLACE_SUB / _WINDOW_SUB, naming its template instance (configs 2 and 4)."""
     import bench
 
-    for op, key, subs, kern in (("regen", "inplace_sub", (1, 4, 2, 0), "k_levels"), ("gauss", "window_sub", (1, 4, 2), "k_window")):
+    for cfg, op, key, subs, kern in [(c, *x) for c in ("c2", "c4") for x in (
+            ("regen", "inplace_sub", (1, 4, 2, 0), "k_levels"), ("gauss", "window_sub", (1, 4, 2), "k_window"))]:
         for sub in subs:
-            rec = bench.latest_inplace_pmc("c2", op, {key: sub})
+            rec = bench.latest_inplace_pmc(cfg, op, {key: sub})
             assert rec is not None and rec["op"] == op and rec[key] == sub, (op, sub)
             assert kern in rec["kernel"] and ("k_levels_x" in rec["kernel"]) == (op == "regen" and sub == 0)
             assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
             assert rec["bench_line_of_traced_run"]["parity"]["status"] == "bit-exact"
     assert bench.latest_inplace_pmc("c2", "regen", {"inplace_sub": 3}) is None
-    assert bench.latest_inplace_pmc("c4", "gauss", {"window_sub": 4}) is None
+    assert bench.latest_inplace_pmc("c3", "gauss", {"window_sub": 4}) is None
+
+
+def test_cpu_baseline_provenance_stamp(tmp_path):
+    """cpu_baseline names the reference text its binary was compiled from:
+    oracle/stamp.py records the sha256 of every source and of the binary; bench._ref_stamp copies it
+    and re-hashes the binary it is about to run; a missing stamp is said, not papered over."""
+    import subprocess
+
+    import bench
+
+    src = tmp_path / "GuassDePyramid.h"
+    src.write_text("// stand-in source text for the stamp test\n")
+    binary = tmp_path / "ref_avx512"
+    binary.write_bytes(b"\x7fELF not really")
+    assert "no stamp" in bench._ref_stamp(str(binary))["status"]
+    subprocess.run([sys.executable, os.path.join(REPO, "oracle", "stamp.py"), str(binary), "g++", "-O2", str(src)],
+                   check=True)
+    st = bench._ref_stamp(str(binary))
+    assert st["binary_matches_stamp"] is True and st["flags"] == "-O2"
+    import hashlib
+
+    assert st["sources_sha256"]["GuassDePyramid.h"] == hashlib.sha256(src.read_bytes()).hexdigest()
+    binary.write_bytes(b"\x7fELF rebuilt without a new stamp")
+    assert bench._ref_stamp(str(binary))["binary_matches_stamp"] is False
