@@ -868,7 +868,7 @@ int gdp_input_halo(gdp_ctx* c, int side, void** rows, size_t* pitch) try {
     }
     *rows = c->d_halo_own[side];
     if (g.halo_ptr[side] == c->d_halo_own[side] && g.halo_rows[side] == n[side] &&
-        g.halo_pitch[side] == c->in_pitch_own)
+        g.halo_pitch[side] == c->in_pitch_own && g.halo_img_stride[side] == (long long)n[side] * c->in_pitch_own)
         return GDP_OK;  // already bound (every exchange asks again): no geometry upload, no drain
     g.halo_ptr[side] = c->d_halo_own[side];
     g.halo_rows[side] = n[side];

@@ -99,6 +99,12 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
         size_t hp = 0;
         for (int side = 0; side < 2; ++side) OK(gdp_input_halo(c, side, &h[side], &hp));
         EXPECT(hp >= (size_t)W && (h[0] != nullptr) == (above > 0) && (h[1] != nullptr) == (below > 0));
+        for (int side = 0; side < 2; ++side) {  // asking again returns the same binding (no re-upload)
+            void* again = nullptr;
+            size_t hp2 = 0;
+            OK(gdp_input_halo(c, side, &again, &hp2));
+            EXPECT(again == h[side] && hp2 == hp);
+        }
         EXPECT(gdp_input_halo(c, 2, &h[0], &hp) != GDP_OK);
         EXPECT(gdp_bind_input_halo(c, h[0], h[1], (size_t)W + 1, 0) != GDP_OK || above + below == 0);  // pitch % 4
         const void* in = nullptr;
@@ -116,9 +122,30 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
     std::vector<uint8_t> u8((size_t)rows * W, 7);
     OK(gdp_set_input_host_u8(c, 0, u8.data(), (size_t)W, nullptr));
     OK(gdp_build(c, nullptr));
-    float tap[4096];
-    OK(gdp_get_taps(c, 0, 0, 0, tap));
-    EXPECT(gdp_get_taps(c, 2, 0, 0, tap) != GDP_OK);
+    // both window centres (one device table each, built on first use) and the row windows of every
+    // octave read back through the layout in use ([row][scale] for non-square images)
+    std::vector<float> tap((size_t)std::max(H, W)), tap2((size_t)std::max(H, W));
+    OK(gdp_get_taps(c, 0, 0, 0, tap.data()));
+    EXPECT(gdp_get_taps(c, 2, 0, 0, tap.data()) != GDP_OK);
+    for (int o = 0; o < go; ++o)
+        for (int sc = 0; sc < S + 3; ++sc) OK(gdp_get_taps(c, 1, o, sc, tap.data()));
+    OK(gdp_get_taps(c, 1, 0, S + 2, tap.data()));
+    for (int rep = 0; rep < 3; ++rep) {
+        OK(gdp_set_window_centre(c, GDP_CENTRE_INTLEN));
+        EXPECT(gdp_get_window_centre(c) == GDP_CENTRE_INTLEN);
+        OK(gdp_build(c, nullptr));
+        OK(gdp_set_window_centre(c, GDP_CENTRE_SERIAL));
+    }
+    OK(gdp_get_taps(c, 1, 0, S + 2, tap2.data()));
+    EXPECT(std::memcmp(tap.data(), tap2.data(), sizeof(float) * (size_t)H) == 0);  // back to the serial table
+    EXPECT(gdp_set_window_centre(c, 7) != GDP_OK);
+    // block tiles refuse a (rows, waves) pair with no kernel instance
+    OK(gdp_set_tuning(c, GDP_TUNE_CONV_KERNEL, 2));
+    OK(gdp_set_tuning(c, GDP_TUNE_CONV_ROWS, 48));
+    OK(gdp_set_tuning(c, GDP_TUNE_CONV_WAVES, 8));
+    if (!band) EXPECT(gdp_build_gaussian(c, nullptr) == GDP_ERR_STATE);
+    OK(gdp_set_tuning(c, GDP_TUNE_CONV_WAVES, 16));
+    OK(gdp_set_tuning(c, GDP_TUNE_CONV_ROWS, 32));
     EXPECT(gdp_device_level(c, 0, go, 0) == nullptr);
     OK(gdp_sync(c));
     gdp_destroy(c);
