@@ -243,6 +243,8 @@ int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
     switch (MODE == 1 ? c->window_sub : c->inplace_sub) {
         case 2: return launch_inplace_sub<MODE, 2>(c, ob, oe, st);
         case 4: return launch_inplace_sub<MODE, 4>(c, ob, oe, st);
+        case 8: return launch_inplace_sub<MODE, 8>(c, ob, oe, st);
+        case 16: return launch_inplace_sub<MODE, 16>(c, ob, oe, st);
         default: return launch_inplace_sub<MODE, 1>(c, ob, oe, st);
     }
 }
@@ -1446,8 +1448,10 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             return GDP_OK;
         case GDP_TUNE_INPLACE_SUB:
         case GDP_TUNE_WINDOW_SUB:
-            if ((value != 1 && value != 2 && value != 4) && !(key == GDP_TUNE_INPLACE_SUB && value == 0))
-                return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2 or 4 (in-place DoG also 0: one level per wave)");
+            if ((value != 1 && value != 2 && value != 4 && value != 8 && value != 16) &&
+                !(key == GDP_TUNE_INPLACE_SUB && value == 0))
+                return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2, 4, 8 or 16 (1024 / sub threads per block; "
+                                              "in-place DoG also 0: one level per wave)");
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
         case GDP_TUNE_CONV_KERNEL:

@@ -58,7 +58,7 @@ def main():
         kv = dict(p.split("=") for p in v.split(","))
         variants.append((v, {"nontemporal": int(kv.get("nt", 1)), "grid": int(kv.get("grid", "0"), 0),
                              "variant": int(kv.get("v", -1)) if "v" in kv else None,
-                             "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1)),
+                             "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1)), "window_sub": int(kv.get("wsub", 4)),
                              "conv_kernel": int(kv.get("ck", 0)), "conv_rows": int(kv.get("cr", 16)),
                              "conv_order": int(kv.get("co", base_conv_order)), "conv_waves": int(kv.get("cw", 16)), "build_lds": int(kv.get("lds", 0))}))
         variants[-1][1]["op"] = kv.get("op", args.op)
