@@ -714,7 +714,7 @@ def main():
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
-    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4],
+    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4, 8, 16],
                     help="--op regen/gauss: force the in-place block shape (GDP_TUNE_INPLACE_SUB / _WINDOW_SUB: "
                          "1024 / N threads, 0 = k_levels_x) and skip its autotune, e.g. for profiling runs")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
@@ -878,7 +878,8 @@ def main():
             c.build(stream)  # materialise the pyramid the in-place passes work on
         steps_fn = [c.generate_dog if args.op == "regen" else (lambda st, c=c: c.gauss_range(0, O, st))
                     for c in ctxs]
-        key, values = ("inplace_sub", [1, 4, 2, 0]) if args.op == "regen" else ("window_sub", [1, 4, 2])
+        key, values = (("inplace_sub", [1, 4, 2, 0, 8, 16]) if args.op == "regen" else
+                       ("window_sub", [1, 4, 2, 8, 16]))
         if args.inplace_sub is not None:
             if args.inplace_sub not in values:
                 sys.exit(f"bench.py: --inplace-sub {args.inplace_sub} is not a {key} value ({values})")

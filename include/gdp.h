@@ -269,10 +269,10 @@ enum {
                                    default chosen from the image width                         */
     GDP_TUNE_TILE_ORDER = 5,    /* build tile order: 0 linear (default), 1 XCD-chunked,
                                    2 XCD row-interleaved                                       */
-    GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk
-                                   (default 4 up to 32 Mpix per launch, else 1; or 2);
-                                   0 = one level per wave (k_levels_x) */
-    GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default, 2 or 1) */
+    GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk,
+                                   1 / 2 / 4 / 8 / 16 (default 16 for one image, else 4 up to
+                                   32 Mpix per launch, else 1); 0 = one level per wave (k_levels_x) */
+    GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default; 1, 2, 8, 16) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (S <= 3), 1 LDS tiles,
                                    2 block tiles (default; one output row per wave, S <= 5) */
     GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian: block tiles' rows per block (32 default;

@@ -476,9 +476,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     try {
     c->device = device;
     c->variant = default_variant(W, (long long)(row_end - row_begin) * W, batch);
-    // in-place re-entry pass (GenerateDoG on the current contents): 256-thread blocks stream best
-    // for launches of up to one 4096^2 image, 1024-thread blocks above (profiles/ab_regen_c*_r02ae.log)
-    c->inplace_sub = (long long)(row_end - row_begin) * W * batch <= (32ll << 20) ? 4 : 1;
+    // in-place re-entry pass (GenerateDoG on the current contents): 64-thread blocks stream best on
+    // single images (4096^2 0.148 vs 0.152 ms for 256 threads, 16384^2 2.37 vs 2.49;
+    // profiles/ab_sub_c*_r03m.log), 256-thread blocks on small batches, 1024-thread above
+    c->inplace_sub = batch == 1 ? 16 : (long long)(row_end - row_begin) * W * batch <= (32ll << 20) ? 4 : 1;
     // Convolution extension default: block tiles of 32 rows (16 waves) in block order 4 (octave-o
     // block rows right after the octave-0 rows that hold their input rows, no XCD chunking) —
     // the fastest form on every config (tools/conv_ab.sh, cold buffers: 4096^2 0.111 ms vs 0.119

@@ -329,7 +329,7 @@ def test_int_star_star_upload(pkg, oracle):
 
 
 # ------------------------------------------------------------------ in-place ops / re-entry
-@pytest.mark.parametrize("sub", [0, 1])
+@pytest.mark.parametrize("sub", [0, 1, 16])
 def test_inplace_ops_match_reference_order(pkg, oracle, sub):
     H, W, S = 72, 104, 2
     O = oracle.default_octaves(H, W)
@@ -352,7 +352,7 @@ def test_inplace_ops_match_reference_order(pkg, oracle, sub):
         _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
 
 
-@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0)])
+@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0), (1, 8), (1, 16)])
 def test_gauss_range_and_store_modes(pkg, oracle, nt, sub):
     """One-launch GaussFilter over an octave range == per-octave GaussFilter; both store modes;
     every in-place DoG kernel (sub 0 = one level per wave, k_levels_x; S = 14 has 17 levels and
@@ -361,7 +361,7 @@ def test_gauss_range_and_store_modes(pkg, oracle, nt, sub):
         O = oracle.default_octaves(H, W)
         imgs = [oracle.lcg_image(H, W, 5 + b) for b in range(B)]
         with pkg.PyramidContext(H, W, S=S, batch=B) as ctx:
-            ctx.set_tuning(nontemporal=nt, inplace_sub=sub, window_sub=4 // min(max(sub, 1), 4))
+            ctx.set_tuning(nontemporal=nt, inplace_sub=sub, window_sub=max(sub, 1))
             for b, img in enumerate(imgs):
                 ctx.set_input(img, b)
             ctx.init()

@@ -7,7 +7,7 @@
 cfg=$1; rnd=${2:-r03}
 steps=()
 for op in regen gauss; do
-  subs="${REGEN_SUBS:-1 4 2 0}"; [ $op = gauss ] && subs="${GAUSS_SUBS:-1 4 2}"
+  subs="${REGEN_SUBS:-1 4 2 0 8 16}"; [ $op = gauss ] && subs="${GAUSS_SUBS:-1 4 2 8 16}"
   for sub in $subs; do
     tag="${cfg}_${op}_s${sub}_${rnd}"
     force="--op ${op} --inplace-sub ${sub} --no-cpu"
