@@ -199,7 +199,7 @@ def test_inplace_traffic_records_name_their_block_shape():
     import bench
 
     for cfg, op, key, subs, kern in [(c, *x) for c in ("c2", "c4") for x in (
-            ("regen", "inplace_sub", (1, 4, 2, 0), "k_levels"), ("gauss", "window_sub", (1, 4, 2), "k_window"))]:
+            ("regen", "inplace_sub", (1, 4, 2, 0, 8, 16), "k_levels"), ("gauss", "window_sub", (1, 4, 2, 8, 16), "k_window"))]:
         for sub in subs:
             rec = bench.latest_inplace_pmc(cfg, op, {key: sub})
             assert rec is not None and rec["op"] == op and rec[key] == sub, (op, sub)
