@@ -256,7 +256,8 @@ def launch_ranks(n, argv, script=None):
     import tempfile
 
     rdv_dir = tempfile.mkdtemp(prefix="gdp_bench_rdv_")
-    log_dir = os.environ.get("GDP_BENCH_RANK_LOGS") or rdv_dir
+    own_logs = not os.environ.get("GDP_BENCH_RANK_LOGS")  # a private log directory: removed unless a rank fails
+    log_dir = tempfile.mkdtemp(prefix="gdp_bench_ranks_") if own_logs else os.environ["GDP_BENCH_RANK_LOGS"]
     os.makedirs(log_dir, exist_ok=True)
     procs, logs = [], []
     for r in range(n):
@@ -305,7 +306,9 @@ def launch_ranks(n, argv, script=None):
                         sys.stderr.write(f.read().decode(errors="replace"))
                 except OSError:
                     pass
-        shutil.rmtree(rdv_dir, ignore_errors=True)
+            if own_logs:
+                shutil.rmtree(log_dir, ignore_errors=True)
+        shutil.rmtree(rdv_dir, ignore_errors=True)  # the failing rank's log (named above) is kept
     return rc
 
 

@@ -93,6 +93,15 @@ def test_bench_launches_its_own_ranks(tmp_path, monkeypatch, capfd):
     assert "rank 1 failing on purpose" in (logs / "rank1.stderr").read_text()
     err = capfd.readouterr().err
     assert "rank 1 exited with 3" in err and "rank 1 failing on purpose" in err and str(logs / "rank1.stderr") in err
+    # without GDP_BENCH_RANK_LOGS the failing rank's log survives in a private directory it names
+    monkeypatch.delenv("GDP_BENCH_RANK_LOGS")
+    assert bench.launch_ranks(2, [str(tmp_path), "fail-rank1"], script=str(probe)) == 3
+    err = capfd.readouterr().err
+    path = err.split("Its stderr (", 1)[1].split(")", 1)[0]
+    assert os.path.exists(path) and "failing on purpose" in open(path).read()
+    import shutil
+
+    shutil.rmtree(os.path.dirname(path))
 
 
 def test_rank_topology_assembly(monkeypatch):
