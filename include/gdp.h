@@ -288,10 +288,7 @@ enum {
                                    pinned staging buffer (32768 default) */
     GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
                                    into the caller's rows (8 default, at most the host's threads) */
-    GDP_TUNE_CONV_WAVES = 15,   /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
-    GDP_TUNE_CONV_SPLIT = 16    /* gdp_build_gaussian block tiles: 1 = octave 0 and octaves >= 1 as two
-                                   concurrent launches (a second stream forked from and joined back
-                                   into the caller's); 0 (default) = one launch */
+    GDP_TUNE_CONV_WAVES = 15    /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

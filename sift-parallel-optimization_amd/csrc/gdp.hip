@@ -97,10 +97,6 @@ struct gdp_ctx {
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
     int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
-    int conv_split = 0;           // GDP_TUNE_CONV_SPLIT: block tiles of octave 0 and of octaves >= 1 as two
-                                  // concurrent launches (second stream, fork / join events)
-    hipStream_t conv_stream2 = nullptr;
-    hipEvent_t conv_fork = nullptr, conv_join = nullptr;
     int conv_order = 4;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
                                   // bit 2 input-row-interleaved octaves (conv_sweep_perm; default 4)
     int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
@@ -363,18 +359,12 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     return hipGetLastError();
 }
 
-// a launch over blocks [vbase, vbase + vper) of each image (ConvRange): every octave, or one octave
-// range on its own stream (gdp_build_gaussian's octave split)
-struct ConvRange {
-    unsigned vbase, vper;
-    int order;
-};
 template <int L, int T, int W>
-hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st, ConvRange r) {
+hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     auto k = k_conv_blk<L, T, W>;
-    const unsigned grid = (r.order & 1) ? (units + 7u) / 8u * 8u : units;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, r.order,
-                       c->d_conv_perm, r.vbase, r.vper);
+    const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
+                       c->d_conv_perm);
     return hipGetLastError();
 }
 
@@ -382,29 +372,29 @@ hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st, ConvRan
 // tile grid (bk_blk) was planned for conv_rows, so any other pair is refused, never run with a
 // different tile height
 template <int L>
-hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st, ConvRange r) {
+hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
     const int T = c->conv_rows, W = c->conv_waves;
     if (W == 8) {
         switch (T) {
-            case 8: return launch_conv_blk_t<L, 8, 8>(c, units, st, r);
-            case 16: return launch_conv_blk_t<L, 16, 8>(c, units, st, r);
-            case 24: return launch_conv_blk_t<L, 24, 8>(c, units, st, r);
-            case 32: return launch_conv_blk_t<L, 32, 8>(c, units, st, r);
+            case 8: return launch_conv_blk_t<L, 8, 8>(c, units, st);
+            case 16: return launch_conv_blk_t<L, 16, 8>(c, units, st);
+            case 24: return launch_conv_blk_t<L, 24, 8>(c, units, st);
+            case 32: return launch_conv_blk_t<L, 32, 8>(c, units, st);
             default: return hipErrorInvalidConfiguration;
         }
     }
     if (W != 16) return hipErrorInvalidConfiguration;
     switch (T) {
-        case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st, r);
-        case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st, r);
-        case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st, r);
+        case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
+        case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
+        case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
         default: return hipErrorInvalidConfiguration;
     }
 }
 
 template <int L>
 hipError_t launch_conv_sweep_l(gdp_ctx* c, unsigned grid, hipStream_t st) {
-    if (c->conv_kernel == 2) return launch_conv_blk<L>(c, grid, st, ConvRange{0, c->geom.bk_blk[c->geom.O], c->conv_order});
+    if (c->conv_kernel == 2) return launch_conv_blk<L>(c, grid, st);
     return conv_sweep_rows(c) == 32 ? launch_conv_sweep_t<L, 32>(c, grid, st) : launch_conv_sweep_t<L, 16>(c, grid, st);
 }
 
@@ -667,12 +657,6 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_ctaps) (void)hipFree(c->d_ctaps);
     if (c->d_cradius) (void)hipFree(c->d_cradius);
     if (c->d_conv_perm) (void)hipFree(c->d_conv_perm);
-    if (c->conv_stream2) {
-        (void)hipStreamSynchronize(c->conv_stream2);
-        (void)hipStreamDestroy(c->conv_stream2);
-    }
-    if (c->conv_fork) (void)hipEventDestroy(c->conv_fork);
-    if (c->conv_join) (void)hipEventDestroy(c->conv_join);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->ev_stage)
         if (e) (void)hipEventDestroy(e);
@@ -992,40 +976,7 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
         if (rc != GDP_OK) return rc;
         c->conv_perm_kernel = c->conv_kernel;
     }
-    const bool split = sweep && c->conv_kernel == 2 && c->conv_split && g.O > 1 && g.bk_blk[1] > 0 &&
-                       g.bk_blk[g.O] > g.bk_blk[1];
-    if (split) {
-        // octave 0 on `st`, octaves >= 1 on a second stream forked from and joined back into `st`:
-        // the two launches run concurrently, so the small one fills the big one's ramp and drain
-        if (!c->conv_stream2) {
-            GDP_HIP(c, hipStreamCreateWithFlags(&c->conv_stream2, hipStreamNonBlocking));
-            GDP_HIP(c, hipEventCreateWithFlags(&c->conv_fork, hipEventDisableTiming));
-            GDP_HIP(c, hipEventCreateWithFlags(&c->conv_join, hipEventDisableTiming));
-        }
-        const unsigned n0 = g.bk_blk[1], nr = g.bk_blk[g.O] - g.bk_blk[1];
-        const int ord = c->conv_order & ~4;
-        if ((long long)(n0 > nr ? n0 : nr) * g.batch >= (1ll << 31) - 8)
-            return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
-        GDP_HIP(c, hipEventRecord(c->conv_fork, st));
-        GDP_HIP(c, hipStreamWaitEvent(c->conv_stream2, c->conv_fork, 0));
-        auto two = [&](auto lc) -> hipError_t {
-            constexpr int L = decltype(lc)::value;
-            hipError_t e = launch_conv_blk<L>(c, nr * (unsigned)g.batch, c->conv_stream2, ConvRange{n0, nr, ord});
-            if (e == hipSuccess) e = launch_conv_blk<L>(c, n0 * (unsigned)g.batch, st, ConvRange{0, n0, ord});
-            return e;
-        };
-        switch (g.L) {
-            case 3: GDP_HIP(c, two(std::integral_constant<int, 3>{})); break;
-            case 4: GDP_HIP(c, two(std::integral_constant<int, 4>{})); break;
-            case 5: GDP_HIP(c, two(std::integral_constant<int, 5>{})); break;
-            case 6: GDP_HIP(c, two(std::integral_constant<int, 6>{})); break;
-            case 7: GDP_HIP(c, two(std::integral_constant<int, 7>{})); break;
-            default: GDP_HIP(c, two(std::integral_constant<int, 8>{})); break;
-        }
-        GDP_HIP(c, hipEventRecord(c->conv_join, c->conv_stream2));
-        GDP_HIP(c, hipStreamWaitEvent(st, c->conv_join, 0));
-    }
-    if (sweep && !split) {
+    if (sweep) {
         const long long grid = (long long)blk[g.O] * g.batch;
         if (grid >= (1ll << 31) - 8) return c->status(GDP_ERR_ARG, "convolution build too large for one launch");
         if (grid > 0) {
@@ -1034,8 +985,8 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
                 case 4: GDP_HIP(c, launch_conv_sweep_l<4>(c, (unsigned)grid, st)); break;
                 case 5: GDP_HIP(c, launch_conv_sweep_l<5>(c, (unsigned)grid, st)); break;
                 case 6: GDP_HIP(c, launch_conv_sweep_l<6>(c, (unsigned)grid, st)); break;
-                case 7: GDP_HIP(c, launch_conv_blk<7>(c, (unsigned)grid, st, ConvRange{0, g.bk_blk[g.O], c->conv_order})); break;
-                default: GDP_HIP(c, launch_conv_blk<8>(c, (unsigned)grid, st, ConvRange{0, g.bk_blk[g.O], c->conv_order})); break;
+                case 7: GDP_HIP(c, launch_conv_blk<7>(c, (unsigned)grid, st)); break;
+                default: GDP_HIP(c, launch_conv_blk<8>(c, (unsigned)grid, st)); break;
             }
         }
     }
@@ -1474,7 +1425,6 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
         case GDP_TUNE_CONV_WAVES: *value = c->conv_waves; return GDP_OK;
-        case GDP_TUNE_CONV_SPLIT: *value = c->conv_split; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -1527,9 +1477,6 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
         case GDP_TUNE_CONV_WAVES:
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
             c->conv_waves = value;
-            return GDP_OK;
-        case GDP_TUNE_CONV_SPLIT:
-            c->conv_split = value ? 1 : 0;
             return GDP_OK;
         case GDP_TUNE_CONV_ORDER:
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");

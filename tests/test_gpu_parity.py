@@ -421,33 +421,6 @@ def test_errors_are_loud(pkg):
         pkg.PyramidContext(32, 32, S=2, octaves=9)
 
 
-def test_conv_octave_split_is_bit_identical(pkg):
-    """GDP_TUNE_CONV_SPLIT: octave 0 and octaves >= 1 of the block tiles as two concurrent launches
-    (a second stream forked from and joined back into the caller's) compute exactly the one-launch
-    bits — the same kernel on disjoint blocks — on a batch and on a row band, on the torch stream."""
-    import torch
-
-    for H, W, B, band in ((512, 480, 2, None), (1024, 512, 1, (256, 768))):
-        kw = dict(row_begin=band[0], row_end=band[1]) if band else {}
-        with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B, **kw) as ctx:
-            ctx.fill_synthetic(11, 0)
-            if band:
-                ctx.set_tuning(conv_kernel=2)
-                above, below = ctx.conv_halo_rows()
-                for side, n in ((0, above), (1, below)):
-                    if n:
-                        ctx.input_halo(side)
-            got = {}
-            st = torch.cuda.Stream()
-            for split in (0, 1):
-                ctx.set_tuning(conv_split=split)
-                ctx.build_gaussian(st)
-                st.synchronize()
-                got[split] = [ctx.pyramid(b) for b in range(B)]
-            for b in range(B):
-                assert np.array_equal(_bits(got[0][b]), _bits(got[1][b])), (H, W, band, b)
-
-
 def test_conv_block_tiles_refuse_uninstantiated_pairs(pkg):
     """the block tiles' grid is planned for conv_rows, so a (rows, waves) pair with no
     kernel instance (48 rows on 8 waves, 8 rows on 16) is refused with an error — never run with
@@ -912,15 +885,13 @@ _CONV_KERNELS = [dict(conv_kernel=0, conv_rows=16, conv_order=0), dict(conv_kern
                  dict(conv_kernel=1), dict(conv_kernel=2, conv_rows=16, conv_order=0),
                  dict(conv_kernel=2, conv_rows=8, conv_waves=8, conv_order=5), dict(conv_kernel=2, conv_rows=32, conv_order=4),
                  dict(conv_kernel=2, conv_rows=48, conv_order=1), dict(conv_kernel=2, conv_rows=24, conv_waves=8, conv_order=4),
-                 dict(conv_kernel=2, conv_rows=32, conv_waves=8, conv_order=1),
-                 dict(conv_kernel=2, conv_rows=32, conv_order=4, conv_split=1)]
+                 dict(conv_kernel=2, conv_rows=32, conv_waves=8, conv_order=1)]
 
 
 @pytest.mark.parametrize("H,W,S,O,fmt,batch", _CONV_SHAPES)
 @pytest.mark.parametrize("tune", _CONV_KERNELS, ids=["sweep16", "sweep32", "sweep16xcd_alt", "sweep32alt",
                                                           "sweep16rowmix", "sweep32rowmix_xcd", "tiles", "blk16",
-                                                          "blk8rowmix_xcd", "blk32rowmix", "blk48xcd", "blk24w8rowmix", "blk32w8xcd",
-                                                          "blk32split"])
+                                                          "blk8rowmix_xcd", "blk32rowmix", "blk48xcd", "blk24w8rowmix", "blk32w8xcd"])
 def test_true_gaussian_convolution_extension(pkg, oracle, H, W, S, O, fmt, batch, tune):
     """Extension mode (no reference counterpart; parity unpinned by construction): checked against
     a float64 separable convolution, for both kernels (register sweep with DPP lane shifts, LDS
