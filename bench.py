@@ -270,6 +270,11 @@ def launch_ranks(n, argv, script=None):
             procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env,
                                           stderr=err))
     rc = 0
+
+    def forward(signum, frame):  # the launcher itself told to stop (timeout, Ctrl-C): stop the ranks too
+        raise SystemExit(128 + signum)
+
+    old_handlers = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
     try:
         live = list(procs)
         while live:
@@ -291,7 +296,14 @@ def launch_ranks(n, argv, script=None):
                     for q in live:
                         q.send_signal(signal.SIGTERM)
             time.sleep(0.05)
+    except BaseException:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        raise
     finally:
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
         for p in procs:
             if p.poll() is None:
                 try:

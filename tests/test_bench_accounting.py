@@ -104,6 +104,40 @@ def test_bench_launches_its_own_ranks(tmp_path, monkeypatch, capfd):
     shutil.rmtree(os.path.dirname(path))
 
 
+def test_launcher_stopped_by_a_signal_stops_its_ranks(tmp_path):
+    """A launcher that is itself told to stop (SIGTERM from a timeout) stops its ranks instead of
+    leaving them running on the GPUs."""
+    import signal
+    import subprocess
+    import time
+
+    sleeper = tmp_path / "sleeper.py"
+    sleeper.write_text("import os, sys, time\nopen(os.path.join(sys.argv[1], 'pid%s' % os.environ['RANK']), 'w')"
+                       ".write(str(os.getpid()))\ntime.sleep(600)\n")
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.launch_ranks(2, [%r], script=%r))" % (REPO, str(tmp_path), str(sleeper)))
+    parent = subprocess.Popen([sys.executable, "-c", code])
+    for _ in range(400):
+        if all((tmp_path / f"pid{r}").exists() and (tmp_path / f"pid{r}").read_text() for r in range(2)):
+            break
+        time.sleep(0.05)
+    pids = [int((tmp_path / f"pid{r}").read_text()) for r in range(2)]
+    parent.send_signal(signal.SIGTERM)
+    assert parent.wait(timeout=60) != 0
+
+    def running(pid):  # gone, or a zombie waiting to be reaped
+        try:
+            with open(f"/proc/{pid}/status") as f:
+                return not any(line.startswith("State:") and "Z" in line for line in f)
+        except OSError:
+            return False
+
+    deadline = time.time() + 10
+    while any(running(p) for p in pids) and time.time() < deadline:
+        time.sleep(0.1)
+    assert not any(running(p) for p in pids), pids
+
+
 def test_rank_topology_assembly(monkeypatch):
     """The N-rank line certifies itself: rank_topology gathers every rank's
     device identity and counts the ranks with an all_reduce of ones.  A gloo rehearsal with two
