@@ -288,10 +288,7 @@ enum {
                                    pinned staging buffer (32768 default) */
     GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
                                    into the caller's rows (8 default, at most the host's threads) */
-    GDP_TUNE_CONV_WAVES = 15,   /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
-    GDP_TUNE_CONV_HALO = 17     /* gdp_build_gaussian block tiles: halo lanes per side, 2 (default:
-                                   240 output columns per tile) or 4 (224 columns, every tile and wave
-                                   store on whole 128-B lines; 32 rows x 16 waves only) */
+    GDP_TUNE_CONV_WAVES = 15    /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

@@ -24,7 +24,7 @@ GDP_INPUT_I32, GDP_INPUT_U8 = 0, 1
 GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT, GDP_TUNE_TILE_ORDER = 1, 2, 3, 4, 5
 GDP_TUNE_INPLACE_SUB, GDP_TUNE_WINDOW_SUB, GDP_TUNE_CONV_KERNEL, GDP_TUNE_CONV_ROWS = 6, 7, 8, 9
 GDP_TUNE_CONV_ORDER, GDP_TUNE_BUILD_LDS, GDP_TUNE_STAGE_KB, GDP_TUNE_STAGE_THREADS = 11, 12, 13, 14
-GDP_TUNE_CONV_WAVES, GDP_TUNE_CONV_HALO = 15, 17
+GDP_TUNE_CONV_WAVES = 15
 
 
 class GdpError(RuntimeError):

@@ -97,8 +97,6 @@ struct gdp_ctx {
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
     int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
-    int conv_halo = 2;            // GDP_TUNE_CONV_HALO: halo lanes per side of the block tiles (2: 240 columns,
-                                  // 4: 224 columns, 128-B aligned tiles; 32 rows x 16 waves only)
     int conv_order = 4;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
                                   // bit 2 input-row-interleaved octaves (conv_sweep_perm; default 4)
     int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
@@ -294,8 +292,7 @@ static bool conv_blk_pair_ok(int rows, int waves) {
 }
 static void conv_sweep_geom(gdp_ctx* c) {
     Geom& g = c->geom;
-    // block tiles with 4 halo lanes per side are 224 columns wide (GDP_TUNE_CONV_HALO); the sweep's strips 240
-    const int strip_cols = (c->conv_kernel == 2 && c->conv_halo == 4) ? kSwV * (64 - 8) : SwGeom<kSwV>::kCols;
+    const int strip_cols = SwGeom<kSwV>::kCols;
     g.sw_blk[0] = 0;
     g.cvx_blk[0] = 0;
     g.bk_blk[0] = 0;
@@ -362,9 +359,9 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int L, int T, int W, int HL = 2>
+template <int L, int T, int W>
 hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
-    auto k = k_conv_blk<L, T, W, HL>;
+    auto k = k_conv_blk<L, T, W>;
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
                        c->d_conv_perm);
@@ -387,7 +384,6 @@ hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
         }
     }
     if (W != 16) return hipErrorInvalidConfiguration;
-    if (c->conv_halo == 4) return T == 32 ? launch_conv_blk_t<L, 32, 16, 4>(c, units, st) : hipErrorInvalidConfiguration;
     switch (T) {
         case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
         case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
@@ -970,8 +966,6 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
         const int r = c->conv_rows, k = c->conv_kernel, w = c->conv_waves;
         if (sweep && k == 0 && r != 16 && r != 32)
             return c->status(GDP_ERR_STATE, "conv rows %d not available for the register sweep (16 or 32)", r);
-        if (sweep && k == 2 && c->conv_halo == 4 && !(r == 32 && w == 16))
-            return c->status(GDP_ERR_STATE, "conv block tiles with 4 halo lanes: 32 rows x 16 waves only");
         if (sweep && k == 2 && !conv_blk_pair_ok(r, w))
             return c->status(GDP_ERR_STATE, "conv block tiles: %d rows with %d waves is not an instantiated pair "
                                             "(16 waves: 16 / 32 / 48 rows; 8 waves: 8 / 16 / 24 / 32 rows)", r, w);
@@ -1431,7 +1425,6 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
         case GDP_TUNE_CONV_WAVES: *value = c->conv_waves; return GDP_OK;
-        case GDP_TUNE_CONV_HALO: *value = c->conv_halo; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -1462,20 +1455,11 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
                                               "in-place DoG also 0: one level per wave)");
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
-        case GDP_TUNE_CONV_KERNEL: {
+        case GDP_TUNE_CONV_KERNEL:
             if (value < 0 || value > 2)
                 return c->status(GDP_ERR_ARG, "conv kernel must be 0 (sweep), 1 (LDS tiles) or 2 (block tiles)");
-            const int old = c->conv_kernel;
             c->conv_kernel = value;
-            if (c->conv_halo == 2) return GDP_OK;  // strip widths do not depend on the kernel
-            conv_sweep_geom(c);
-            const int rc = upload_geom(c);
-            if (rc != GDP_OK) {
-                c->conv_kernel = old;
-                conv_sweep_geom(c);
-            }
-            return rc;
-        }
+            return GDP_OK;
         case GDP_TUNE_CONV_ROWS: {
             if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48)
                 return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32 or 48 (sweep: 16 / 32; block tiles: "
@@ -1494,18 +1478,6 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
             c->conv_waves = value;
             return GDP_OK;
-        case GDP_TUNE_CONV_HALO: {
-            if (value != 2 && value != 4) return c->status(GDP_ERR_ARG, "conv halo lanes must be 2 or 4");
-            const int old = c->conv_halo;
-            c->conv_halo = value;
-            conv_sweep_geom(c);
-            const int rc = upload_geom(c);
-            if (rc != GDP_OK) {
-                c->conv_halo = old;
-                conv_sweep_geom(c);
-            }
-            return rc;
-        }
         case GDP_TUNE_CONV_ORDER:
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;

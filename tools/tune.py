@@ -60,7 +60,7 @@ def main():
                              "variant": int(kv.get("v", -1)) if "v" in kv else None,
                              "tile_order": int(kv.get("ord", 0)), "inplace_sub": int(kv.get("sub", 1)), "window_sub": int(kv.get("wsub", 4)),
                              "conv_kernel": int(kv.get("ck", 0)), "conv_rows": int(kv.get("cr", 16)),
-                             "conv_order": int(kv.get("co", base_conv_order)), "conv_waves": int(kv.get("cw", 16)), "conv_halo": int(kv.get("ch", 2)), "build_lds": int(kv.get("lds", 0))}))
+                             "conv_order": int(kv.get("co", base_conv_order)), "conv_waves": int(kv.get("cw", 16)), "build_lds": int(kv.get("lds", 0))}))
         variants[-1][1]["op"] = kv.get("op", args.op)
         if variants[-1][1]["variant"] is None:
             del variants[-1][1]["variant"]
