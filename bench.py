@@ -1016,7 +1016,8 @@ def main():
                         "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks)%s"
                                  % (1024 // tun["window_sub"], " (autotuned)" if autotuned else ""),
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
-                                 "240-column block tiles, one output row per wave, DPP lane shifts)" % ctx.tuning()["conv_rows"]
+                                 "240-column block tiles on %d waves, DPP lane shifts)"
+                                 % (ctx.tuning()["conv_rows"], ctx.tuning().get("conv_waves") or 16)
                                  if ctx.tuning()["conv_kernel"] == 2 and S <= 5 else
                                  "k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
                                  "DPP lane shifts, %d-row strips)" % ctx.tuning()["conv_rows"]
