@@ -792,7 +792,10 @@ int gdp_set_input_format(gdp_ctx* c, int fmt) try {
     void* fresh = nullptr;
     hipError_t e = hipMalloc(&fresh, std::max<size_t>(16, bytes));
     if (e != hipSuccess) return c->status(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, "hipMalloc(input)");
-    GDP_HIP(c, hipMemset(fresh, 0, std::max<size_t>(16, bytes)));
+    if ((e = hipMemset(fresh, 0, std::max<size_t>(16, bytes))) != hipSuccess) {
+        (void)hipFree(fresh);
+        return c->status(GDP_ERR_HIP, "hipMemset(input): %s", hipGetErrorString(e));
+    }
     GDP_HIP(c, hipFree(c->d_in_own));
     c->d_in_own = fresh;
     c->geom.in_fmt = fmt;

@@ -8,12 +8,24 @@ form (oracle/gdp_oracle.c, pinned to the reference's own outputs by tests/test_o
 for word, including signs of zero and subnormals.  The seed is fixed, so a failure names a
 reproducible case.
 """
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 300
+# GDP_FUZZ_SCALE multiplies every sweep's case count and GDP_FUZZ_SEED offsets its seed, for
+# one-off long sweeps on hardware (profiles/fuzz_*.log); the suite runs the defaults
+SCALE = max(1, int(os.environ.get("GDP_FUZZ_SCALE", "1")))
+SEED = int(os.environ.get("GDP_FUZZ_SEED", "0"))
+N_CASES = 300 * SCALE
+INPLACE_SUBS = (0, 1, 2, 4, 8, 16)
+
+
+def _progress(name, i):
+    if SCALE > 1 and i % 100 == 0:  # long sweeps: a line every 100 cases (visible with -s)
+        print(f"{name}: case {i}", flush=True)
 
 
 def _bits(a):
@@ -30,7 +42,7 @@ def _case(rng):
     fmt = "u8" if rng.random() < 0.3 else "i32"
     device_input = rng.random() < 0.3
     variant = int(rng.integers(0, 19))
-    order = int(rng.integers(0, 2))
+    order = int(rng.integers(0, 3))
     bands = rng.random() < 0.25 and B == 1 and not device_input
     return H, W, S, O, B, fmt, device_input, variant, order, bands
 
@@ -44,17 +56,32 @@ def _images(rng, H, W, B, fmt):
     return [rng.integers(lo, hi, size=(H, W), dtype=np.int64).astype(np.int32) for _ in range(B)]
 
 
+def _follow_up(rng):
+    """What runs after the build (whole-image cases): nothing, the GenerateDoG re-entry (in-place,
+    random block split) or the GaussFilter pass of a random octave range."""
+    r = rng.random()
+    kind = "none" if r < 0.6 else "regen" if r < 0.85 else "gauss"
+    return kind, int(rng.choice(INPLACE_SUBS)), int(rng.choice(INPLACE_SUBS[1:]))
+
+
 def test_randomized_parity_sweep(pkg, oracle):
+    """... plus, per case, the window centre (the serial float-halved one or the MPI variants'
+    integer-length one) and, on whole images, a follow-up in-place pass checked after it."""
     import torch
 
-    rng = np.random.default_rng(20261016)
+    rng = np.random.default_rng(20261016 + SEED)
     for i in range(N_CASES):
+        _progress("build", i)
         H, W, S, O, B, fmt, device_input, variant, order, bands = _case(rng)
+        centre = "intlen" if rng.random() < 0.3 else "serial"
+        follow, isub, wsub = _follow_up(rng)
+        if centre == "intlen" and follow == "gauss":
+            follow = "regen"  # the oracle's per-octave GaussFilter restates the serial centre only
         imgs = _images(rng, H, W, B, fmt)
         Oeff = O or oracle.default_octaves(H, W)
-        wants = [oracle.build_pyramid(img.astype(np.int32), S, Oeff) for img in imgs]
+        wants = [oracle.build_pyramid(img.astype(np.int32), S, Oeff, centre=centre) for img in imgs]
         what = dict(case=i, H=H, W=W, S=S, O=O, B=B, fmt=fmt, device_input=device_input, variant=variant,
-                    order=order, bands=bands)
+                    order=order, bands=bands, centre=centre, follow=follow, isub=isub, wsub=wsub)
         if bands:
             align = 1 << (max(Oeff, 5) - 1)
             cuts = sorted({0, H} | {c for c in range(align, H, align) if rng.random() < 0.5})
@@ -63,6 +90,7 @@ def test_randomized_parity_sweep(pkg, oracle):
             for r0, r1 in zip(cuts[:-1], cuts[1:]):
                 with pkg.PyramidContext(H, W, S=S, octaves=O, row_begin=r0, row_end=r1, input_format=fmt) as ctx:
                     ctx.set_tuning(variant=variant, tile_order=order)
+                    ctx.set_window_centre(centre)
                     ctx.set_input(imgs[0][r0:r1])
                     ctx.build()
                     for o in range(Oeff):
@@ -74,7 +102,8 @@ def test_randomized_parity_sweep(pkg, oracle):
                 assert np.array_equal(_bits(got[k]), _bits(want[k])), (what, k)
             continue
         with pkg.PyramidContext(H, W, S=S, octaves=O, batch=B, input_format=fmt) as ctx:
-            ctx.set_tuning(variant=variant, tile_order=order)
+            ctx.set_tuning(variant=variant, tile_order=order, inplace_sub=isub, window_sub=wsub)
+            ctx.set_window_centre(centre)
             if device_input:
                 pitch = W + int(rng.integers(0, 9))
                 host = np.zeros((B, H, pitch), imgs[0].dtype)
@@ -88,6 +117,18 @@ def test_randomized_parity_sweep(pkg, oracle):
                 for b in range(B):
                     ctx.set_input(imgs[b], b)
                 ctx.build()
+            if follow == "regen":
+                ctx.generate_dog()
+                for w in wants:
+                    oracle.generate_dog(w, H, W, S, Oeff, centre=centre)
+            elif follow == "gauss":
+                ob = int(rng.integers(0, Oeff))
+                oe = int(rng.integers(ob + 1, Oeff + 1))
+                ctx.gauss_range(ob, oe)
+                for w in wants:
+                    for o in range(ob, oe):
+                        oracle.gauss_octave(w, H, W, S, o)
+                what["octaves"] = (ob, oe)
             for b in range(B):
                 got = ctx.pyramid(b)
                 assert got.shape == wants[b].shape, what
@@ -96,7 +137,7 @@ def test_randomized_parity_sweep(pkg, oracle):
 
 
 # ---- GenerateDoG_nomp_dynamic's subset (the AVX-512 x OpenMP header's semantics) ----------------
-N_SUBSET_CASES = 120
+N_SUBSET_CASES = 120 * SCALE
 
 
 def test_randomized_subset_sweep(pkg, oracle):
@@ -104,8 +145,9 @@ def test_randomized_subset_sweep(pkg, oracle):
     shapes / S / octave counts / batches / formats / variants / tile orders / row bands, against
     the oracle's restatement (pinned to the header run here by tests/test_oracle.py), with the
     header's integer-length window centre."""
-    rng = np.random.default_rng(20261017)
+    rng = np.random.default_rng(20261017 + SEED)
     for i in range(N_SUBSET_CASES):
+        _progress("subset", i)
         H, W, S, O, B, fmt, _, variant, order, bands = _case(rng)
         again = rng.random() < 0.5
         imgs = _images(rng, H, W, B, fmt)
@@ -152,7 +194,7 @@ def test_randomized_subset_sweep(pkg, oracle):
 
 
 # ---- the convolution extension (no reference counterpart) -------------------------------------
-N_CONV_CASES = 120
+N_CONV_CASES = 120 * SCALE
 _CONV_TUNES = [dict(conv_kernel=2, conv_rows=32, conv_order=4), dict(conv_kernel=2, conv_rows=16, conv_order=0),
                dict(conv_kernel=2, conv_rows=48, conv_order=5), dict(conv_kernel=2, conv_rows=24, conv_waves=8, conv_order=1),
                dict(conv_kernel=2, conv_rows=8, conv_waves=8, conv_order=4), dict(conv_kernel=0, conv_rows=16, conv_order=5),
@@ -188,8 +230,9 @@ def test_randomized_convolution_sweep(pkg, oracle):
     import torch
 
     d = importlib.import_module(pkg.__name__ + ".distributed")
-    rng = np.random.default_rng(20261017)
+    rng = np.random.default_rng(20261017 + SEED)
     for i in range(N_CONV_CASES):
+        _progress("conv", i)
         H = int(rng.integers(1, 401))
         W = int(rng.integers(1, 401)) if rng.random() < 0.6 else int(rng.integers(1, 13)) * 32
         S = int(rng.integers(0, 5))
