@@ -15,10 +15,12 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-# GDP_FUZZ_SCALE multiplies every sweep's case count and GDP_FUZZ_SEED offsets its seed, for
+# GDP_FUZZ_SCALE multiplies every sweep's case count, GDP_FUZZ_SEED offsets its seed and
+# GDP_FUZZ_MAXDIM raises the build / subset sweeps' largest side (300), for
 # one-off long sweeps on hardware (profiles/fuzz_*.log); the suite runs the defaults
 SCALE = max(1, int(os.environ.get("GDP_FUZZ_SCALE", "1")))
 SEED = int(os.environ.get("GDP_FUZZ_SEED", "0"))
+MAXDIM = max(300, int(os.environ.get("GDP_FUZZ_MAXDIM", "300")))  # shapes 1..MAXDIM (build / subset)
 N_CASES = 300 * SCALE
 INPLACE_SUBS = (0, 1, 2, 4, 8, 16)
 
@@ -33,8 +35,8 @@ def _bits(a):
 
 
 def _case(rng):
-    H = int(rng.integers(1, 301))
-    W = int(rng.integers(1, 301))
+    H = int(rng.integers(1, MAXDIM + 1))
+    W = int(rng.integers(1, MAXDIM + 1))
     S = int(rng.integers(0, 5))
     omax = max(1, int(np.floor(np.log2(min(H, W)))) + 1)
     O = 0 if rng.random() < 0.5 else int(rng.integers(1, omax + 1))
