@@ -725,8 +725,7 @@ def main():
     ap.add_argument("--variant", type=int, default=None,
                     help="force a build-kernel variant (and skip autotuning), e.g. for profiling runs")
     ap.add_argument("--tile-order", type=int, default=None,
-                    help="with --variant: force the build tile order too (0 linear, 1 XCD-chunked, 2 XCD row-interleaved, "
-                         "3 per-image tails)")
+                    help="with --variant: force the build tile order too (0 linear, 1 XCD-chunked)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")

@@ -268,8 +268,7 @@ enum {
     GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile shape), 0..18;
                                    default chosen from the image width                         */
     GDP_TUNE_TILE_ORDER = 5,    /* build tile order: 0 linear (default), 1 XCD-chunked,
-                                   2 XCD row-interleaved, 3 linear with each image's tail
-                                   units (octaves >= F) right after its own tiles              */
+                                   2 XCD row-interleaved                                       */
     GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk,
                                    1 / 2 / 4 / 8 / 16 (default 16 for one image, else 4 up to
                                    32 Mpix per launch, else 1); 0 = one level per wave (k_levels_x) */

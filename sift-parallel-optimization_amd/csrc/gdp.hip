@@ -166,22 +166,14 @@ int retile(gdp_ctx* c, int tile_cols, int tile_rows) {
     if (tail_per_img * g.batch >= (1ll << 31)) return c->status(GDP_ERR_ARG, "image/batch too large for one context");
     g.tail_groups_per_img = (unsigned)tail_per_img;
     g.tail_units = (unsigned)tail_units;
-    g.tail_units_img = (int)((tail_per_img + kTailGroups - 1) / kTailGroups);
     g.tiles_r = (g.in_rows + tile_rows - 1) / tile_rows;
     g.tiles_c = (g.W + tile_cols - 1) / tile_cols;
     const long long tiles_per_img = (long long)g.tiles_r * g.tiles_c;
-    if ((tiles_per_img + g.tail_units_img) * g.batch >= (1ll << 31))
+    if (tiles_per_img * g.batch + g.tail_units >= (1ll << 31))
         return c->status(GDP_ERR_ARG, "image/batch too large for one context (split the batch)");
     g.tiles_per_img = (unsigned)tiles_per_img;
     g.tiles_total = (unsigned)(tiles_per_img * g.batch);
     return GDP_OK;
-}
-
-// Work units of one build launch: the tiles, then the tail units (flattened over the batch), or
-// with tile order 3 each image's tiles followed by that image's own tail units.
-long long build_units(const Geom& g) {
-    return g.tile_order == 3 ? (long long)(g.tiles_per_img + (unsigned)g.tail_units_img) * g.batch
-                             : (long long)g.tiles_total + g.tail_units;
 }
 
 // Geometry changes are configuration-time events: drain the device first so no in-flight launch
@@ -195,7 +187,7 @@ int upload_geom(gdp_ctx* c) {
 
 int launch_build(gdp_ctx* c, hipStream_t st, bool subset = false) {
     const Geom& g = c->geom;
-    const long long units = build_units(g);
+    const long long units = (long long)g.tiles_total + g.tail_units;
     if (units == 0) return GDP_OK;
     // default: one unit per block; GDP_TUNE_GRID / GDP_TUNE_BLOCKS_PER_CU cap it (persistent loop)
     const long long cap = c->grid_override > 0 ? c->grid_override : (c->persistent ? c->blocks_max : units);
@@ -1506,7 +1498,7 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             c->stage_threads = value;
             return GDP_OK;
         case GDP_TUNE_TILE_ORDER:
-            if (value < 0 || value > 3) return c->status(GDP_ERR_ARG, "tile order must be 0, 1, 2 or 3");
+            if (value < 0 || value > 2) return c->status(GDP_ERR_ARG, "tile order must be 0, 1 or 2");
             c->geom.tile_order = value;
             return upload_geom(c);
         case GDP_TUNE_VARIANT: {

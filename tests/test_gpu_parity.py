@@ -156,36 +156,11 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
         want = oracle.build_pyramid(img, S, O or None)
         with pkg.PyramidContext(H, W, S=S, octaves=O) as ctx:
             ctx.set_input(img)
-            for kw in ({"variant": variant}, {"tile_order": 1}, {"tile_order": 2}, {"tile_order": 3}, {"nontemporal": 0},
+            for kw in ({"variant": variant}, {"tile_order": 1}, {"tile_order": 2}, {"nontemporal": 0},
                        {"blocks_per_cu": 1}, {"grid": 3}, {"blocks_per_cu": 0, "grid": 0, "build_lds": 41984}):
                 ctx.set_tuning(**kw)
                 ctx.build()
                 _assert_same(ctx.pyramid(0), want, (variant, H, W, S, O, kw))
-
-
-@pytest.mark.parametrize("variant", [7, 8, 11, 16, 15])
-def test_per_image_tail_order_on_batches(pkg, oracle, variant):
-    """Tile order 3 (each image's tail units — the octaves a tile does not fuse — right after its
-    own tiles) on batches whose per-image tail range is not a multiple of a unit, one unit per
-    block and on a capped grid, full and subset semantics."""
-    H, W, S, B = 200, 300, 2, 3
-    imgs = [oracle.lcg_image(H, W, 900 + b) for b in range(B)]
-    want = [oracle.build_pyramid(im, S, None) for im in imgs]
-    with pkg.PyramidContext(H, W, S=S, batch=B) as ctx:
-        for b, im in enumerate(imgs):
-            ctx.set_input(im, b)
-        for kw in ({"variant": variant, "tile_order": 3}, {"grid": 5}, {"grid": 0, "blocks_per_cu": 1}):
-            ctx.set_tuning(**kw)
-            ctx.build()
-            for b in range(B):
-                _assert_same(ctx.pyramid(b), want[b], (variant, b, kw))
-        ctx.set_tuning(blocks_per_cu=0, grid=0)
-        ctx.set_window_centre("intlen")
-        ctx.build_subset()
-        for b, im in enumerate(imgs):
-            w = oracle.init_pyramid(im, S, None)
-            oracle.subset_a512omp(w, H, W, S, oracle.default_octaves(H, W))
-            _assert_same(ctx.pyramid(b), w, (variant, "subset", b))
 
 
 def test_default_variant_follows_geometry(pkg):
