@@ -66,12 +66,26 @@ def main():
             del variants[-1][1]["variant"]
         if "bpc" in kv:
             variants[-1][1]["blocks_per_cu"] = int(kv["bpc"])
+        if "ip" in kv or "is" in kv:  # timing-only: read a caller buffer with this input pitch / image stride
+            ip = int(kv.get("ip", W))
+            variants[-1][1]["in_layout"] = (ip, int(kv.get("is", H * ip)))
     times = {name: [] for name, _ in variants}
 
+    padded = {}
+
     def apply(kw):  # fresh context state per variant: persistent only when bpc is given
-        for c in ctxs:
-            c.set_tuning(**{k: v for k, v in kw.items() if k not in ("blocks_per_cu", "op")})
+        for i, c in enumerate(ctxs):
+            c.set_tuning(**{k: v for k, v in kw.items() if k not in ("blocks_per_cu", "op", "in_layout")})
             c.set_tuning(blocks_per_cu=kw.get("blocks_per_cu", 0))
+            if "in_layout" in kw:  # random pixels in a padded layout (timing only: needs --no-check)
+                import torch
+                ip, istride = kw["in_layout"]
+                key = (i, ip, istride)
+                if key not in padded:
+                    padded[key] = torch.randint(0, 256, (B * istride + 64,), dtype=torch.int32, device="cuda")
+                c.bind_device_input(padded[key].data_ptr(), ip, istride, keepalive=padded[key])
+            elif c._bound is not None:
+                c.unbind_device_input()
 
     for name, kw in variants:  # warm-up + identical-output check for every variant (per op)
         apply(kw)
