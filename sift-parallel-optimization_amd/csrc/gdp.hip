@@ -515,6 +515,9 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // one cold line per scale: 65536 x 4096 builds in 1.227 vs 1.43-1.46 ms (v15), 16384 x 4096 in
     // 0.315 vs 0.363 ms — the speed of row windows that are always hot (timing-only build, 1.25
     // ms); config 3 and the in-place passes unchanged (profiles/ab_rowtap_r03c.log, bit-exact)
+    // timing-only experiment (round 3): output rows of every level at a power-of-two pitch; only
+    // k_build writes with it, every other op and reader assumes pitch = cols (wrong values)
+    const char* out_pitch_env = std::getenv("GDP_OUT_PITCH");
     const char* rl_env = std::getenv("GDP_ROWTAP_LAYOUT");
     const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : true;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
@@ -527,7 +530,12 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         og.rows = std::max(0, row_hi - og.row0);
         og.cols = W >> o;
         og.gpr = (og.cols + 3) / 4;
-        og.lev_stride = round_up((long long)og.rows * og.cols, kLevelAlign) + level_pad;
+        og.pitch = og.cols;
+        if (out_pitch_env && std::atoi(out_pitch_env) == 1)  // timing only: k_build alone honours it
+            while (og.pitch & (og.pitch - 1)) og.pitch += og.pitch & -og.pitch;
+        else if (out_pitch_env && std::atoi(out_pitch_env) > 1)  // or cols + N floats (N multiple of 4)
+            og.pitch += (std::atoi(out_pitch_env) >> o) & ~3;
+        og.lev_stride = round_up((long long)og.rows * og.pitch, kLevelAlign) + level_pad;
         og.lev_off = lev_off;
         lev_off += og.lev_stride * g.L;
         og.ctap_stride = (int)round_up(og.cols, 4);
