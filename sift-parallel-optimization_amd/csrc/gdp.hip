@@ -518,6 +518,12 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // timing-only experiment (round 3): output rows of every level at a power-of-two pitch; only
     // k_build writes with it, every other op and reader assumes pitch = cols (wrong values)
     const char* out_pitch_env = std::getenv("GDP_OUT_PITCH");
+    // layout experiment (round 3): level and image-pyramid strides rounded up to this many floats
+    // (a power of two >= 64; default 64 = 256 B) — the values stay right (every reader takes the
+    // offsets from the geometry)
+    const char* align_env = std::getenv("GDP_LEVEL_ALIGN");
+    long long lev_align = align_env ? std::atoll(align_env) : kLevelAlign;
+    if (lev_align < kLevelAlign || (lev_align & (lev_align - 1))) lev_align = kLevelAlign;
     const char* rl_env = std::getenv("GDP_ROWTAP_LAYOUT");
     const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : true;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
@@ -535,7 +541,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
             while (og.pitch & (og.pitch - 1)) og.pitch += og.pitch & -og.pitch;
         else if (out_pitch_env && std::atoi(out_pitch_env) > 1)  // or cols + N floats (N multiple of 4)
             og.pitch += (std::atoi(out_pitch_env) >> o) & ~3;
-        og.lev_stride = round_up((long long)og.rows * og.pitch, kLevelAlign) + level_pad;
+        og.lev_stride = round_up((long long)og.rows * og.pitch, lev_align) + level_pad;
         og.lev_off = lev_off;
         lev_off += og.lev_stride * g.L;
         og.ctap_stride = (int)round_up(og.cols, 4);
@@ -571,7 +577,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         g.cv_tiles_c[o] = (og.cols + kCvTW - 1) / kCvTW;
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
-    g.pyr_stride = round_up(lev_off, kLevelAlign);
+    g.pyr_stride = round_up(lev_off, lev_align);
     const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
     const long long tail_units = (tail_per_img * batch + kTailGroups - 1) / kTailGroups;
     const long long min_tiles = (long long)((g.in_rows + kTileRows - 1) / kTileRows) * ((W + 63) / 64) * batch;
