@@ -515,15 +515,6 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // one cold line per scale: 65536 x 4096 builds in 1.227 vs 1.43-1.46 ms (v15), 16384 x 4096 in
     // 0.315 vs 0.363 ms — the speed of row windows that are always hot (timing-only build, 1.25
     // ms); config 3 and the in-place passes unchanged (profiles/ab_rowtap_r03c.log, bit-exact)
-    // timing-only experiment (round 3): output rows of every level at a power-of-two pitch; only
-    // k_build writes with it, every other op and reader assumes pitch = cols (wrong values)
-    const char* out_pitch_env = std::getenv("GDP_OUT_PITCH");
-    // layout experiment (round 3): level and image-pyramid strides rounded up to this many floats
-    // (a power of two >= 64; default 64 = 256 B) — the values stay right (every reader takes the
-    // offsets from the geometry)
-    const char* align_env = std::getenv("GDP_LEVEL_ALIGN");
-    long long lev_align = align_env ? std::atoll(align_env) : kLevelAlign;
-    if (lev_align < kLevelAlign || (lev_align & (lev_align - 1))) lev_align = kLevelAlign;
     const char* rl_env = std::getenv("GDP_ROWTAP_LAYOUT");
     const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : true;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
@@ -536,12 +527,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         og.rows = std::max(0, row_hi - og.row0);
         og.cols = W >> o;
         og.gpr = (og.cols + 3) / 4;
-        og.pitch = og.cols;
-        if (out_pitch_env && std::atoi(out_pitch_env) == 1)  // timing only: k_build alone honours it
-            while (og.pitch & (og.pitch - 1)) og.pitch += og.pitch & -og.pitch;
-        else if (out_pitch_env && std::atoi(out_pitch_env) > 1)  // or cols + N floats (N multiple of 4)
-            og.pitch += (std::atoi(out_pitch_env) >> o) & ~3;
-        og.lev_stride = round_up((long long)og.rows * og.pitch, lev_align) + level_pad;
+        og.lev_stride = round_up((long long)og.rows * og.cols, kLevelAlign) + level_pad;
         og.lev_off = lev_off;
         lev_off += og.lev_stride * g.L;
         og.ctap_stride = (int)round_up(og.cols, 4);
@@ -577,7 +563,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         g.cv_tiles_c[o] = (og.cols + kCvTW - 1) / kCvTW;
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
-    g.pyr_stride = round_up(lev_off, lev_align);
+    g.pyr_stride = round_up(lev_off, kLevelAlign);
     const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
     const long long tail_units = (tail_per_img * batch + kTailGroups - 1) / kTailGroups;
     const long long min_tiles = (long long)((g.in_rows + kTileRows - 1) / kTileRows) * ((W + 63) / 64) * batch;
