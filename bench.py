@@ -190,10 +190,10 @@ def latest_conv_pmc(config_key, tun):
     return best
 
 
-def latest_pmc(config_key, variant, tile_order, op="build", levels=5):
+def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
-    whose recorded build variant and tile order equal the run's; None when no profile of that
+    whose recorded build variant, tile order and zero-window mode equal the run's; None when no profile of that
     instance exists (the traffic of another variant would describe a different kernel)."""
     pdir = os.path.join(REPO, "profiles")
     best = None
@@ -210,6 +210,7 @@ def latest_pmc(config_key, variant, tile_order, op="build", levels=5):
                 if rec.get("config") == config_key and rec.get("op", "build") == op and \
                         rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
                         rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32" and \
+                        rec.get("zero_window", 0) == zero_window and \
                         lt in rec.get("kernel", lt):
                     best = dict(rec, file=f)
     return best
@@ -360,7 +361,8 @@ def rank_topology(world, rank, local, backend, dist, args):
 
 
 def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
-    """gdp_autotune's search (every build variant x tile order 0/1) over the ROTATED step sequence
+    """gdp_autotune's search (every build variant x tile order 0/1, and for the full build x
+    zero-window mode 0/1: GDP_TUNE_ZERO_WINDOW) over the ROTATED step sequence
     the benchmark times (one set when it alone exceeds the MALL), so the pick is made on cold
     buffers; candidates are interleaved round-robin over `rounds` rounds and ranked by their
     median (drift hits all alike, unlike gdp_autotune's one-candidate-at-a-time timing).  All
@@ -376,12 +378,12 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
             ctxs[0].set_tuning(variant=v)
         except pkg.GdpError:
             break
-        cands += [(v, 0), (v, 1)]
+        cands += [(v, o, z) for z in ((0, 1) if op == "build" else (0,)) for o in (0, 1)]
     times = {c: [] for c in cands}
     for _ in range(rounds):
-        for v, order in cands:
+        for v, order, zw in cands:
             for c in ctxs:
-                c.set_tuning(variant=v, tile_order=order)
+                c.set_tuning(variant=v, tile_order=order, zero_window=zw)
             run = [c.build_subset if op == "subset" else c.build for c in ctxs]
             for r in run:
                 r(stream)
@@ -391,11 +393,11 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
                 run[i % len(ctxs)](stream)
             e1.record(stream)
             e1.synchronize()
-            times[(v, order)].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
+            times[(v, order, zw)].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
     med = {c: sorted(t)[len(t) // 2] for c, t in times.items()}
     best = min(cands, key=lambda c: med[c])
     for c in ctxs:
-        c.set_tuning(variant=best[0], tile_order=best[1])
+        c.set_tuning(variant=best[0], tile_order=best[1], zero_window=best[2])
     return best[0], best[1], med[best]
 
 
@@ -726,6 +728,9 @@ def main():
                     help="force a build-kernel variant (and skip autotuning), e.g. for profiling runs")
     ap.add_argument("--tile-order", type=int, default=None,
                     help="with --variant: force the build tile order too (0 linear, 1 XCD-chunked)")
+    ap.add_argument("--zero-window", type=int, default=None, choices=[0, 1],
+                    help="with --variant: force GDP_TUNE_ZERO_WINDOW too (outside-support groups skip their window "
+                         "loads; the autotune otherwise picks it)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
@@ -862,7 +867,7 @@ def main():
     autotuned = None
     if args.variant is not None:
         for c in ctxs:
-            c.set_tuning(variant=args.variant, tile_order=args.tile_order)
+            c.set_tuning(variant=args.variant, tile_order=args.tile_order, zero_window=args.zero_window)
     elif args.op in ("build", "subset") and not args.no_autotune:
         # candidates interleaved round-robin (drift hits all alike), over the rotated sets
         autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10, op=args.op)
@@ -964,7 +969,8 @@ def main():
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
     tun = ctx.tuning()
     # PMC records are of the whole workload on one GPU: a row band (config 5 at N > 1) is another launch
-    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3)
+    pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3,
+                      tun["zero_window"] if args.op == "build" else 0)
            if args.op in ("build", "subset") and args.input == "i32" and not (cfg["band"] and world > 1) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
@@ -1002,10 +1008,11 @@ def main():
                                   f"{pmc['conv_order']}) on this workload" if args.op == "conv" else
                                   f"kernel instance (inplace_sub {pmc['inplace_sub']}) on this workload" if args.op == "regen" else
                                   f"kernel instance (window_sub {pmc['window_sub']}) on this workload" if args.op == "gauss" else
-                                  f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}) on this workload")
+                                  f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}, zero window "
+                                  f"{pmc.get('zero_window', 0)}) on this workload")
                                if pmc else "no PMC profile of this kernel instance (variant/tile order) on this workload"),
-            "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d%s"
-                       % (ctx.tuning()["variant"], ctx.tuning()["tile_order"], " (autotuned)" if autotuned else "")
+            "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d, zero window %d%s"
+                       % (tun["variant"], tun["tile_order"], tun["zero_window"], " (autotuned)" if autotuned else "")
                        if args.op == "build" else
                        "k_build<SUB> (fused decimate+window+DoG, GenerateDoG_nomp_dynamic's subset of levels), "
                        "variant %d, tile order %d" % (ctx.tuning()["variant"], ctx.tuning()["tile_order"])

@@ -288,7 +288,11 @@ enum {
                                    pinned staging buffer (32768 default) */
     GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
                                    into the caller's rows (8 default, at most the host's threads) */
-    GDP_TUNE_CONV_WAVES = 15    /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
+    GDP_TUNE_CONV_WAVES = 15,   /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
+    GDP_TUNE_ZERO_WINDOW = 16   /* gdp_build: 1 = 4-pixel groups outside the support of every
+                                   window (all taps of their row or columns +0, any scale, either
+                                   centre) store their DoG levels as +0 before their input lands
+                                   and level S+2 as copysign(0, x); the same bits either way */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

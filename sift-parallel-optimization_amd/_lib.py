@@ -25,6 +25,7 @@ GDP_TUNE_NONTEMPORAL, GDP_TUNE_BLOCKS_PER_CU, GDP_TUNE_GRID, GDP_TUNE_VARIANT, G
 GDP_TUNE_INPLACE_SUB, GDP_TUNE_WINDOW_SUB, GDP_TUNE_CONV_KERNEL, GDP_TUNE_CONV_ROWS = 6, 7, 8, 9
 GDP_TUNE_CONV_ORDER, GDP_TUNE_BUILD_LDS, GDP_TUNE_STAGE_KB, GDP_TUNE_STAGE_THREADS = 11, 12, 13, 14
 GDP_TUNE_CONV_WAVES = 15
+GDP_TUNE_ZERO_WINDOW = 16
 
 
 class GdpError(RuntimeError):

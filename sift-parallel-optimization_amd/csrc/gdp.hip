@@ -97,6 +97,8 @@ struct gdp_ctx {
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
     int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
+    int zero_window = 0;          // GDP_TUNE_ZERO_WINDOW: build groups outside the windows' support store
+                                  // their input-independent levels without waiting for the input
     int conv_order = 4;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
                                   // bit 2 input-row-interleaved octaves (conv_sweep_perm; default 4)
     int build_lds = 0;            // GDP_TUNE_BUILD_LDS: dynamic LDS bytes per build block (caps blocks per CU)
@@ -265,6 +267,41 @@ void fill_host_taps(gdp_ctx* c, int mode) {
             const int n = host_taps(g.H, o, s, rows.data(), mode);  // [row][scale] interleaved
             for (int r = 0; r < n; ++r) c->h_taps[og.rtap + (size_t)r * og.rtap_row + s] = rows[r];
         }
+    }
+}
+
+// Window support of every octave (OctGeom::nz_*): the smallest global row / column ranges that
+// hold every non-zero tap of any scale under EITHER window centre (so switching centres, a tap-
+// table pointer swap, needs no geometry change).  The reference's windows underflow to +0 a few
+// σ from the centre (expf(-d²/(2σ²)) = 0 for d >= 29 at σ = 2), so on a large image almost every
+// pixel lies outside them.  `on` = 0: the ranges cover the whole octave (every group computed).
+void set_window_support(gdp_ctx* c, bool on) {
+    Geom& g = c->geom;
+    for (int o = 0; o < g.O; ++o) {
+        OctGeom& og = g.oct[o];
+        const int Hg = g.H >> o;
+        og.nz_r0 = 0;
+        og.nz_r1 = Hg;
+        og.nz_c0 = 0;
+        og.nz_c1 = og.cols;
+        if (!on) continue;
+        auto support = [&](int length, int& lo, int& hi) {
+            std::vector<float> t((size_t)std::max(1, length >> o));
+            lo = INT32_MAX;
+            hi = 0;
+            for (int mode : {GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN})
+                for (int s = 0; s < g.L; ++s) {
+                    const int n = host_taps(length, o, s, t.data(), mode);
+                    for (int i = 0; i < n; ++i)
+                        if (t[i] != 0.0f) {
+                            lo = std::min(lo, i);
+                            hi = std::max(hi, i + 1);
+                        }
+                }
+            if (lo > hi) lo = hi = 0; // no non-zero tap at all: every pixel is outside
+        };
+        support(g.W, og.nz_c0, og.nz_c1);
+        support(g.H, og.nz_r0, og.nz_r1);
     }
 }
 
@@ -582,6 +619,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     conv_sweep_geom(c);
     c->h_taps.assign((size_t)tap_off, 0.0f);
     fill_host_taps(c, c->centre_mode);
+    set_window_support(c, c->zero_window != 0);
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -1380,33 +1418,39 @@ int gdp_sync(gdp_ctx* c) try {
 void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* best_order, float* best_ms) try {
-    // Times every build-kernel variant x tile order on the context's current input (HIP events on
-    // `stream`, median of 3 repeats of `iters` launches) and keeps the fastest.  All candidates
-    // produce identical bits, so this only ever changes speed.
+    // Times every build-kernel variant x tile order x zero-window mode on the context's current
+    // input (HIP events on `stream`, median of 3 repeats of `iters` launches) and keeps the
+    // fastest.  All candidates produce identical bits, so this only ever changes speed.
     if (!c || iters <= 0) return c ? c->status(GDP_ERR_ARG, "gdp_autotune: iters must be > 0") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     const int old_variant = c->variant, old_order = c->geom.tile_order;
-    int bv = old_variant, bo = old_order;
+    int bv = old_variant, bo = old_order, bz = c->zero_window;
     float bt = 3.4e38f;
-    for (int v = 0; v < kNumVariants; ++v) {
-        for (int ord = 0; ord <= 1; ++ord) {
-            int rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, v);
-            if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, ord);
-            if (rc != GDP_OK) return rc;
-            float t[3];
-            rc = gdp_time_builds(c, 1, stream, &t[0]);  // warm-up
-            for (int r = 0; r < 3 && rc == GDP_OK; ++r) rc = gdp_time_builds(c, iters, stream, &t[r]);
-            if (rc != GDP_OK) return rc;
-            std::sort(t, t + 3);
-            if (t[1] < bt) {
-                bt = t[1];
-                bv = v;
-                bo = ord;
+    for (int zw = 0; zw <= 1; ++zw) {
+        int rc = gdp_set_tuning(c, GDP_TUNE_ZERO_WINDOW, zw);
+        if (rc != GDP_OK) return rc;
+        for (int v = 0; v < kNumVariants; ++v) {
+            for (int ord = 0; ord <= 1; ++ord) {
+                rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, v);
+                if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, ord);
+                if (rc != GDP_OK) return rc;
+                float t[3];
+                rc = gdp_time_builds(c, 1, stream, &t[0]);  // warm-up
+                for (int r = 0; r < 3 && rc == GDP_OK; ++r) rc = gdp_time_builds(c, iters, stream, &t[r]);
+                if (rc != GDP_OK) return rc;
+                std::sort(t, t + 3);
+                if (t[1] < bt) {
+                    bt = t[1];
+                    bv = v;
+                    bo = ord;
+                    bz = zw;
+                }
             }
         }
     }
     int rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, bv);
     if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, bo);
+    if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_ZERO_WINDOW, bz);
     if (rc != GDP_OK) return rc;
     if (best_variant) *best_variant = bv;
     if (best_order) *best_order = bo;
@@ -1428,6 +1472,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_CONV_ROWS: *value = c->conv_rows; return GDP_OK;
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
         case GDP_TUNE_CONV_WAVES: *value = c->conv_waves; return GDP_OK;
+        case GDP_TUNE_ZERO_WINDOW: *value = c->zero_window; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -1481,6 +1526,18 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
             c->conv_waves = value;
             return GDP_OK;
+        case GDP_TUNE_ZERO_WINDOW: {
+            const int old = c->zero_window;
+            if (value != 0 && value != 1) return c->status(GDP_ERR_ARG, "zero window must be 0 or 1");
+            c->zero_window = value;
+            set_window_support(c, c->zero_window != 0);
+            const int rc = upload_geom(c);
+            if (rc != GDP_OK) {
+                c->zero_window = old;
+                set_window_support(c, old != 0);
+            }
+            return rc;
+        }
         case GDP_TUNE_CONV_ORDER:
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;

@@ -189,6 +189,52 @@ def test_large_value_and_negative_inputs(pkg, oracle):
     _assert_same(_gpu_pyramid(pkg, img, 2), oracle.build_pyramid(img, 2), "wide-range ints")
 
 
+@pytest.mark.parametrize("zw", [0, 1])
+def test_zero_window_path_is_bit_exact(pkg, oracle, zw):
+    """GDP_TUNE_ZERO_WINDOW: groups outside every window's support store +0 DoG levels before their
+    input lands and copysign(0, x) as level S+2.  Same bits as the oracle with the knob on and off:
+    negative and zero pixels (the -0.0 of level S+2), wide-range ints, every variant, both window
+    centres, row bands, uint8 input, batches, S = 0..5, odd and non-square shapes."""
+    rng = np.random.default_rng(11)
+    cases = [(300, 500, 2, 0), (257, 1001, 3, 5), (1080, 1920, 2, 5), (200, 200, 0, 0), (129, 255, 5, 0),
+             (64, 96, 2, 0), (33, 700, 1, 0)]
+    for H, W, S, O in cases:
+        img = rng.integers(-2**31, 2**31 - 1, size=(H, W), dtype=np.int64).astype(np.int32)
+        img[::3] = rng.integers(-300, 300, size=img[::3].shape)
+        img[:, ::7] = 0
+        for centre in ("serial", "intlen"):
+            want = oracle.build_pyramid(img, S, O or None, centre=centre)
+            with pkg.PyramidContext(H, W, S=S, octaves=O, centre=centre) as ctx:
+                ctx.set_tuning(zero_window=zw)
+                assert ctx.tuning()["zero_window"] == zw
+                ctx.set_input(img)
+                for v in (15, 16, 11, 0, 9, 4):
+                    ctx.set_tuning(variant=v)
+                    ctx.build()
+                    _assert_same(ctx.pyramid(0), want, ("zero window", zw, H, W, S, O, centre, v))
+    # row bands (global row windows) and a batch of uint8 images
+    H, W = 1024, 768
+    img = rng.integers(-1000, 1000, size=(H, W)).astype(np.int32)
+    want = oracle.levels(oracle.build_pyramid(img, 2, 5), H, W, 2, 5)
+    for r0, r1 in [(0, 256), (256, 512), (512, 1024)]:
+        with pkg.PyramidContext(H, W, S=2, octaves=5, row_begin=r0, row_end=r1) as ctx:
+            ctx.set_tuning(zero_window=zw)
+            ctx.set_input(img[r0:r1])
+            ctx.build()
+            for o in range(5):
+                rows, cols, first = ctx.level_dims(o)
+                for s in range(5):
+                    _assert_same(ctx.level(0, o, s), want[(o, s)][first:first + rows], ("zw band", zw, r0, o, s))
+    imgs = [oracle.lcg_image(300, 400, 70 + b).astype(np.uint8) for b in range(3)]
+    with pkg.PyramidContext(300, 400, S=2, batch=3, input_format="u8") as ctx:
+        ctx.set_tuning(zero_window=zw)
+        for b, im in enumerate(imgs):
+            ctx.set_input(im, b)
+        ctx.build()
+        for b, im in enumerate(imgs):
+            _assert_same(ctx.pyramid(b), oracle.build_pyramid(im.astype(np.int32), 2), ("zw u8", zw, b))
+
+
 # ------------------------------------------------------------------ batch / band / device input
 def test_batched_build(pkg, oracle):
     H, W, B = 120, 200, 5

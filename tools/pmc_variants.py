@@ -37,6 +37,7 @@ def run(args):
     ctxs = [pkg.PyramidContext(H, W, S=2, octaves=O, batch=B) for _ in range(rotate)]
     for c in ctxs:
         c.fill_synthetic(bench.SEED, 0)
+        c.set_tuning(zero_window=args.zero_window)
         if args.op == "subset":  # bench.py --op subset's contexts
             c.set_window_centre("intlen")
         c.sync()
@@ -61,7 +62,8 @@ def run(args):
     for c in ctxs:
         c.close()
     with open(args.manifest, "w") as f:
-        json.dump({"config": args.config, "op": args.op, "rotate": rotate, "instances": manifest}, f)
+        json.dump({"config": args.config, "op": args.op, "rotate": rotate, "zero_window": args.zero_window,
+                   "instances": manifest}, f)
 
 
 def per_dispatch(d, counter):
@@ -93,6 +95,7 @@ def summarise(args):
         write_b = statistics.median(v for _, v, _ in ws) * 1024
         rec = {"config": man["config"], "round": args.round, "kernel": fs[0][2], "variant": m["variant"],
                "tile_order": m["tile_order"], "input_format": "i32", "op": man.get("op", "build"),
+               "zero_window": man.get("zero_window", 0),
                "source": "tools/pmc_variants.py: every instance in one process, its own FETCH_SIZE and WRITE_SIZE "
                          "rocprofv3 --pmc passes, launches cycling over %d cold buffer sets as in bench.py" % man["rotate"],
                "dispatches_counted": [len(fs), len(ws)],
@@ -102,7 +105,8 @@ def summarise(args):
                "traffic_over_algorithmic": (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads); write = WRITE_SIZE KiB"}
         tag = man["config"] + ("_subset" if man.get("op") == "subset" else "")
-        out = os.path.join(REPO, "profiles", f"pmc_{tag}_v{m['variant']}o{m['tile_order']}_{args.round}.json")
+        zw = "z1" if man.get("zero_window", 0) else ""
+        out = os.path.join(REPO, "profiles", f"pmc_{tag}_v{m['variant']}o{m['tile_order']}{zw}_{args.round}.json")
         if os.path.exists(out) and not args.overwrite:
             print("keep", out)
             continue
@@ -120,6 +124,8 @@ def main():
     ap.add_argument("--summarise", action="store_true")
     ap.add_argument("--op", default="build", choices=["build", "subset"],
                     help="subset: the GenerateDoG_nomp_dynamic build (bench.py --op subset)")
+    ap.add_argument("--zero-window", type=int, default=0, choices=[0, 1],
+                    help="GDP_TUNE_ZERO_WINDOW of every instance (records pmc_<cfg>_v<V>o<T>z1_*.json)")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--round", default="r02")

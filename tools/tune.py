@@ -64,6 +64,7 @@ def main():
         variants[-1][1]["op"] = kv.get("op", args.op)
         if variants[-1][1]["variant"] is None:
             del variants[-1][1]["variant"]
+        variants[-1][1]["zero_window"] = int(kv.get("zw", 0))  # every variant sets it (apply() keeps state)
         if "bpc" in kv:
             variants[-1][1]["blocks_per_cu"] = int(kv["bpc"])
         if "ip" in kv or "is" in kv:  # timing-only: read a caller buffer with this input pitch / image stride
