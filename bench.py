@@ -231,7 +231,7 @@ def latest_inplace_pmc(config_key, op, tun):
             except (OSError, ValueError):
                 continue
             if rec.get("config") == config_key and rec.get("op") == op and rec.get("kernel_bytes_per_launch") and \
-                    rec.get(key) == tun[key]:
+                    rec.get(key) == tun[key] and rec.get("zero_window", 0) == tun.get("zero_window", 0):
                 best = dict(rec, file=f)
     return best
 
@@ -405,14 +405,17 @@ def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
     """The in-place passes' block shape (GDP_TUNE_INPLACE_SUB / _WINDOW_SUB: 1024 / 512 / 256-thread
     blocks, or k_levels_x) chosen like the build variant: every candidate timed over the ROTATED
     cold step sequence, interleaved round-robin over `rounds`, median wins.  Bit-identical
-    outputs; the best shape depends on the workload (profiles/ab_regen_c*_r02ae.log)."""
+    outputs; the best shape depends on the workload (profiles/ab_regen_c*_r02ae.log).  Every shape
+    runs with GDP_TUNE_ZERO_WINDOW off and on (profiles/zwi_*_r03an.log): the pick is a pair."""
     import torch
 
-    times = {v: [] for v in values}
+    cands = [(v, z) for v in values for z in (0, 1)]
+    times = {cand: [] for cand in cands}
     for _ in range(rounds):
-        for v in values:
+        for cand in cands:
+            v, z = cand
             for c in ctxs:
-                c.set_tuning(**{key: v})
+                c.set_tuning(**{key: v}, zero_window=z)
             for f in steps_fn:
                 f(stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -421,11 +424,11 @@ def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
                 steps_fn[i % len(ctxs)](stream)
             e1.record(stream)
             e1.synchronize()
-            times[v].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
-    best = min(values, key=lambda v: sorted(times[v])[len(times[v]) // 2])
+            times[cand].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
+    best = min(cands, key=lambda cand: sorted(times[cand])[len(times[cand]) // 2])
     for c in ctxs:
-        c.set_tuning(**{key: best})
-    return best
+        c.set_tuning(**{key: best[0]}, zero_window=best[1])
+    return best[0]
 
 
 def scatter_split(ctx, cfg, world, rank, dist, mg, backend, in_fmt):
@@ -729,8 +732,8 @@ def main():
     ap.add_argument("--tile-order", type=int, default=None,
                     help="with --variant: force the build tile order too (0 linear, 1 XCD-chunked)")
     ap.add_argument("--zero-window", type=int, default=None, choices=[0, 1],
-                    help="with --variant: force GDP_TUNE_ZERO_WINDOW too (outside-support groups skip their window "
-                         "loads; the autotune otherwise picks it)")
+                    help="with --variant / --inplace-sub: force GDP_TUNE_ZERO_WINDOW too (groups outside every "
+                         "window's support skip their window loads; the autotunes otherwise pick it)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
@@ -904,7 +907,7 @@ def main():
             if args.inplace_sub not in values:
                 sys.exit(f"bench.py: --inplace-sub {args.inplace_sub} is not a {key} value ({values})")
             for c in ctxs:
-                c.set_tuning(**{key: args.inplace_sub})
+                c.set_tuning(**{key: args.inplace_sub}, zero_window=args.zero_window)
         elif not args.no_autotune:
             autotuned = (key, autotune_inplace(ctxs, steps_fn, stream, 3 if B * H * W > (1 << 28) else 10, key, values))
     n_step = [0]
@@ -1006,8 +1009,10 @@ def main():
             "traffic_source": (f"profiles/{pmc['file']}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same "
                                + (f"kernel instance (conv kernel {pmc['conv_kernel']}, rows {pmc['conv_rows']}, order "
                                   f"{pmc['conv_order']}) on this workload" if args.op == "conv" else
-                                  f"kernel instance (inplace_sub {pmc['inplace_sub']}) on this workload" if args.op == "regen" else
-                                  f"kernel instance (window_sub {pmc['window_sub']}) on this workload" if args.op == "gauss" else
+                                  f"kernel instance (inplace_sub {pmc['inplace_sub']}, zero window {pmc.get('zero_window', 0)}) "
+                                  f"on this workload" if args.op == "regen" else
+                                  f"kernel instance (window_sub {pmc['window_sub']}, zero window {pmc.get('zero_window', 0)}) "
+                                  f"on this workload" if args.op == "gauss" else
                                   f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}, zero window "
                                   f"{pmc.get('zero_window', 0)}) on this workload")
                                if pmc else "no PMC profile of this kernel instance (variant/tile order) on this workload"),
@@ -1019,9 +1024,10 @@ def main():
                        if args.op == "subset" else
                        {"regen": ("k_levels_x (in-place window+DoG, one level per wave)" if tun["inplace_sub"] == 0 else
                                   "k_levels<MODE=3> (in-place window+DoG, all octaves, %d-thread blocks)"
-                                  % (1024 // tun["inplace_sub"])) + (" (autotuned)" if autotuned else ""),
-                        "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks)%s"
-                                 % (1024 // tun["window_sub"], " (autotuned)" if autotuned else ""),
+                                  % (1024 // tun["inplace_sub"])) + ", zero window %d" % tun["zero_window"]
+                                 + (" (autotuned)" if autotuned else ""),
+                        "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks), zero window %d%s"
+                                 % (1024 // tun["window_sub"], tun["zero_window"], " (autotuned)" if autotuned else ""),
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
                                  "240-column block tiles on %d waves, DPP lane shifts)"
                                  % (ctx.tuning()["conv_rows"], ctx.tuning().get("conv_waves") or 16)

@@ -289,10 +289,12 @@ enum {
     GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
                                    into the caller's rows (8 default, at most the host's threads) */
     GDP_TUNE_CONV_WAVES = 15,   /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
-    GDP_TUNE_ZERO_WINDOW = 16   /* gdp_build: 1 = 4-pixel groups outside the support of every
-                                   window (all taps of their row or columns +0, any scale, either
-                                   centre) store their DoG levels as +0 before their input lands
-                                   and level S+2 as copysign(0, x); the same bits either way */
+    GDP_TUNE_ZERO_WINDOW = 16   /* 1 = 4-pixel groups outside the support of every window (all
+                                   taps of their row or columns +0, any scale, either centre) skip
+                                   their window loads: gdp_build stores their DoG levels as +0
+                                   before the input lands and level S+2 as copysign(0, x); the
+                                   in-place window passes (gdp_generate_dog, gdp_gauss_*) form
+                                   v * 0.0f.  The same bits either way; 0 (default) off */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--inplace-sub", type=int, default=None,
                     help="--op regen: GDP_TUNE_INPLACE_SUB the profiled runs were forced to (0 = k_levels_x)")
     ap.add_argument("--window-sub", type=int, default=None, help="--op gauss: GDP_TUNE_WINDOW_SUB of the profiled runs")
+    ap.add_argument("--zero-window", type=int, default=0, help="GDP_TUNE_ZERO_WINDOW of the profiled runs")
     ap.add_argument("--tag", default=None, help="file tag (default: config, or config_op)")
     args = ap.parse_args()
     if args.op in ("build", "subset") and (args.variant is None or args.tile_order is None):
@@ -80,6 +81,7 @@ def main():
         "variant": args.variant, "tile_order": args.tile_order, "input_format": "i32",
         **({"inplace_sub": args.inplace_sub} if args.inplace_sub is not None else {}),
         **({"window_sub": args.window_sub} if args.window_sub is not None else {}),
+        "zero_window": args.zero_window,
         "trace_calls": int(stats["Calls"]) if stats else None,
         "trace_avg_ns": float(stats["AverageNs"]) if stats else None,
         "trace_min_ns": float(stats["MinNs"]) if stats else None,

@@ -212,9 +212,11 @@ def test_traffic_records_match_only_their_kernel_instance():
     for cfg in ("c2", "c3", "c4", "c5"):
         for v in range(19):
             for t in (0, 1):
-                rec = bench.latest_pmc(cfg, v, t)
-                assert rec is not None and rec["variant"] == v and rec["tile_order"] == t, (cfg, v, t)
-                assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
+                for zw in (0, 1):  # the autotune also picks GDP_TUNE_ZERO_WINDOW
+                    rec = bench.latest_pmc(cfg, v, t, zero_window=zw)
+                    assert rec is not None and rec["variant"] == v and rec["tile_order"] == t, (cfg, v, t, zw)
+                    assert rec.get("zero_window", 0) == zw, (cfg, v, t, zw)
+                    assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
     assert bench.latest_pmc("c2", 99, 0) is None
     conv = bench.latest_conv_pmc("c2", {"conv_kernel": 2, "conv_rows": 32, "conv_order": 4})
     assert conv is not None and conv["op"] == "conv"
@@ -243,9 +245,10 @@ def test_inplace_traffic_records_name_their_block_shape():
 
     for cfg, op, key, subs, kern in [(c, *x) for c in ("c2", "c4") for x in (
             ("regen", "inplace_sub", (1, 4, 2, 0, 8, 16), "k_levels"), ("gauss", "window_sub", (1, 4, 2, 8, 16), "k_window"))]:
-        for sub in subs:
-            rec = bench.latest_inplace_pmc(cfg, op, {key: sub})
-            assert rec is not None and rec["op"] == op and rec[key] == sub, (op, sub)
+        for sub, zw in [(sub, zw) for sub in subs for zw in (0, 1)]:  # the autotune also picks the zero window
+            rec = bench.latest_inplace_pmc(cfg, op, {key: sub, "zero_window": zw})
+            assert rec is not None and rec["op"] == op and rec[key] == sub, (op, sub, zw)
+            assert rec.get("zero_window", 0) == zw, (cfg, op, sub, zw)
             assert kern in rec["kernel"] and ("k_levels_x" in rec["kernel"]) == (op == "regen" and sub == 0)
             assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
             assert rec["bench_line_of_traced_run"]["parity"]["status"] == "bit-exact"

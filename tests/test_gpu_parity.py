@@ -212,6 +212,21 @@ def test_zero_window_path_is_bit_exact(pkg, oracle, zw):
                     ctx.set_tuning(variant=v)
                     ctx.build()
                     _assert_same(ctx.pyramid(0), want, ("zero window", zw, H, W, S, O, centre, v))
+                # the in-place window passes on the current contents (re-entry): k_levels, k_levels_x, k_window
+                Oo = O or oracle.default_octaves(H, W)
+                re = want.copy()
+                oracle.generate_dog(re, H, W, S, Oo, centre=centre)
+                win = re.copy()
+                for o in range(Oo):  # (the oracle's GaussFilter has the serial centre only)
+                    oracle.gauss_octave(win, H, W, S, o)
+                for sub, wsub in ((1, 4), (0, 1), (4, 16)):
+                    ctx.set_tuning(inplace_sub=sub, window_sub=wsub)
+                    ctx.build()
+                    ctx.generate_dog()
+                    _assert_same(ctx.pyramid(0), re, ("zero window re-entry", zw, H, W, S, O, centre, sub))
+                    if centre == "serial":
+                        ctx.gauss_range(0, ctx.O)
+                        _assert_same(ctx.pyramid(0), win, ("zero window GaussFilter", zw, H, W, S, O, wsub))
     # row bands (global row windows) and a batch of uint8 images
     H, W = 1024, 768
     img = rng.integers(-1000, 1000, size=(H, W)).astype(np.int32)
