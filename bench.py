@@ -362,7 +362,8 @@ def rank_topology(world, rank, local, backend, dist, args):
 
 def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
     """gdp_autotune's search (every build variant x tile order 0/1, and for the full build x
-    zero-window mode 0/1: GDP_TUNE_ZERO_WINDOW) over the ROTATED step sequence
+    store mode: (GDP_TUNE_ZERO_WINDOW, GDP_TUNE_STORE_PACE) in (0, off) (0, 1) (1, off) (1, 0)) over the
+    ROTATED step sequence
     the benchmark times (one set when it alone exceeds the MALL), so the pick is made on cold
     buffers; candidates are interleaved round-robin over `rounds` rounds and ranked by their
     median (drift hits all alike, unlike gdp_autotune's one-candidate-at-a-time timing).  All
@@ -378,12 +379,13 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
             ctxs[0].set_tuning(variant=v)
         except pkg.GdpError:
             break
-        cands += [(v, o, z) for z in ((0, 1) if op == "build" else (0,)) for o in (0, 1)]
+        modes = ((0, -1), (0, 1), (1, -1), (1, 0)) if op == "build" else ((0, -1),)
+        cands += [(v, o, z, p) for z, p in modes for o in (0, 1)]
     times = {c: [] for c in cands}
     for _ in range(rounds):
-        for v, order, zw in cands:
+        for v, order, zw, sp in cands:
             for c in ctxs:
-                c.set_tuning(variant=v, tile_order=order, zero_window=zw)
+                c.set_tuning(variant=v, tile_order=order, zero_window=zw, store_pace=sp)
             run = [c.build_subset if op == "subset" else c.build for c in ctxs]
             for r in run:
                 r(stream)
@@ -393,11 +395,11 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
                 run[i % len(ctxs)](stream)
             e1.record(stream)
             e1.synchronize()
-            times[(v, order, zw)].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
+            times[(v, order, zw, sp)].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
     med = {c: sorted(t)[len(t) // 2] for c, t in times.items()}
     best = min(cands, key=lambda c: med[c])
     for c in ctxs:
-        c.set_tuning(variant=best[0], tile_order=best[1], zero_window=best[2])
+        c.set_tuning(variant=best[0], tile_order=best[1], zero_window=best[2], store_pace=best[3])
     return best[0], best[1], med[best]
 
 
@@ -734,6 +736,8 @@ def main():
     ap.add_argument("--zero-window", type=int, default=None, choices=[0, 1],
                     help="with --variant / --inplace-sub: force GDP_TUNE_ZERO_WINDOW too (groups outside every "
                          "window's support skip their window loads; the autotunes otherwise pick it)")
+    ap.add_argument("--store-pace", type=int, default=None, choices=[-1, 0, 1, 2, 3],
+                    help="with --variant: force GDP_TUNE_STORE_PACE too (-1 off; n: s_waitcnt vmcnt(n) after each store)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
@@ -870,7 +874,8 @@ def main():
     autotuned = None
     if args.variant is not None:
         for c in ctxs:
-            c.set_tuning(variant=args.variant, tile_order=args.tile_order, zero_window=args.zero_window)
+            c.set_tuning(variant=args.variant, tile_order=args.tile_order, zero_window=args.zero_window,
+                         store_pace=args.store_pace)
     elif args.op in ("build", "subset") and not args.no_autotune:
         # candidates interleaved round-robin (drift hits all alike), over the rotated sets
         autotuned = autotune_rotating(ctxs, stream, 3 if B * H * W > (1 << 28) else 10, op=args.op)
@@ -1014,10 +1019,12 @@ def main():
                                   f"kernel instance (window_sub {pmc['window_sub']}, zero window {pmc.get('zero_window', 0)}) "
                                   f"on this workload" if args.op == "gauss" else
                                   f"kernel instance (variant {pmc['variant']}, tile order {pmc['tile_order']}, zero window "
-                                  f"{pmc.get('zero_window', 0)}) on this workload")
+                                  f"{pmc.get('zero_window', 0)}) on this workload (store pacing waits change no bytes)")
                                if pmc else "no PMC profile of this kernel instance (variant/tile order) on this workload"),
-            "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d, zero window %d%s"
-                       % (tun["variant"], tun["tile_order"], tun["zero_window"], " (autotuned)" if autotuned else "")
+            "kernel": ("k_build (fused decimate+window+DoG), variant %d, tile order %d, zero window %d, store pace %s%s"
+                       % (tun["variant"], tun["tile_order"], tun["zero_window"],
+                          "off" if tun["store_pace"] < 0 else "vmcnt(%d)" % tun["store_pace"],
+                          " (autotuned)" if autotuned else "")
                        if args.op == "build" else
                        "k_build<SUB> (fused decimate+window+DoG, GenerateDoG_nomp_dynamic's subset of levels), "
                        "variant %d, tile order %d" % (ctx.tuning()["variant"], ctx.tuning()["tile_order"])

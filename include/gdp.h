@@ -289,12 +289,16 @@ enum {
     GDP_TUNE_STAGE_THREADS = 14, /* row-pointer downloads: host threads scattering a staged batch
                                    into the caller's rows (8 default, at most the host's threads) */
     GDP_TUNE_CONV_WAVES = 15,   /* gdp_build_gaussian block tiles: waves per block (16 default, 8) */
-    GDP_TUNE_ZERO_WINDOW = 16   /* 1 = 4-pixel groups outside the support of every window (all
+    GDP_TUNE_ZERO_WINDOW = 16,  /* 1 = 4-pixel groups outside the support of every window (all
                                    taps of their row or columns +0, any scale, either centre) skip
                                    their window loads: gdp_build stores their DoG levels as +0
                                    before the input lands and level S+2 as copysign(0, x); the
                                    in-place window passes (gdp_generate_dog, gdp_gauss_*) form
                                    v * 0.0f.  The same bits either way; 0 (default) off */
+    GDP_TUNE_STORE_PACE = 17    /* -1 (default) off; n = 0..3: after each pyramid store of the
+                                   convolution block tiles and of the build's outside-support
+                                   groups, wait until at most n memory operations of the wave are
+                                   outstanding (A/B knob; the same bits either way) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order on the context's current input (`iters`

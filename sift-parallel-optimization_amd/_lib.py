@@ -26,6 +26,7 @@ GDP_TUNE_INPLACE_SUB, GDP_TUNE_WINDOW_SUB, GDP_TUNE_CONV_KERNEL, GDP_TUNE_CONV_R
 GDP_TUNE_CONV_ORDER, GDP_TUNE_BUILD_LDS, GDP_TUNE_STAGE_KB, GDP_TUNE_STAGE_THREADS = 11, 12, 13, 14
 GDP_TUNE_CONV_WAVES = 15
 GDP_TUNE_ZERO_WINDOW = 16
+GDP_TUNE_STORE_PACE = 17
 
 
 class GdpError(RuntimeError):

@@ -541,6 +541,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     g.in_pitch = round_up(W, 4);
     g.in_img_stride = (long long)g.in_rows * g.in_pitch;
     g.vec_in = 1;
+    g.store_pace = -1;
     c->in_pitch_own = g.in_pitch;
     c->in_img_stride_own = g.in_img_stride;
 
@@ -1418,16 +1419,21 @@ int gdp_sync(gdp_ctx* c) try {
 void* gdp_stream(const gdp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* best_order, float* best_ms) try {
-    // Times every build-kernel variant x tile order x zero-window mode on the context's current
-    // input (HIP events on `stream`, median of 3 repeats of `iters` launches) and keeps the
-    // fastest.  All candidates produce identical bits, so this only ever changes speed.
+    // Times every build-kernel variant x tile order x store mode on the context's current input
+    // (HIP events on `stream`, median of 3 repeats of `iters` launches) and keeps the fastest.
+    // Store modes (zero window, store pace): (0, off), (0, 1), (1, off), (1, 0) — the pairs that won
+    // somewhere in profiles/sp*_r03a{p,q}.log.  All candidates produce identical bits, so this only
+    // ever changes speed.
     if (!c || iters <= 0) return c ? c->status(GDP_ERR_ARG, "gdp_autotune: iters must be > 0") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     const int old_variant = c->variant, old_order = c->geom.tile_order;
-    int bv = old_variant, bo = old_order, bz = c->zero_window;
+    int bv = old_variant, bo = old_order, bz = c->zero_window, bp = c->geom.store_pace;
     float bt = 3.4e38f;
-    for (int zw = 0; zw <= 1; ++zw) {
+    static const int kModes[4][2] = {{0, -1}, {0, 1}, {1, -1}, {1, 0}};
+    for (const auto& mode : kModes) {
+        const int zw = mode[0], sp = mode[1];
         int rc = gdp_set_tuning(c, GDP_TUNE_ZERO_WINDOW, zw);
+        if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_STORE_PACE, sp);
         if (rc != GDP_OK) return rc;
         for (int v = 0; v < kNumVariants; ++v) {
             for (int ord = 0; ord <= 1; ++ord) {
@@ -1444,6 +1450,7 @@ int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* be
                     bv = v;
                     bo = ord;
                     bz = zw;
+                    bp = sp;
                 }
             }
         }
@@ -1451,6 +1458,7 @@ int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* be
     int rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, bv);
     if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, bo);
     if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_ZERO_WINDOW, bz);
+    if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_STORE_PACE, bp);
     if (rc != GDP_OK) return rc;
     if (best_variant) *best_variant = bv;
     if (best_order) *best_order = bo;
@@ -1473,6 +1481,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_CONV_ORDER: *value = c->conv_order; return GDP_OK;
         case GDP_TUNE_CONV_WAVES: *value = c->conv_waves; return GDP_OK;
         case GDP_TUNE_ZERO_WINDOW: *value = c->zero_window; return GDP_OK;
+        case GDP_TUNE_STORE_PACE: *value = c->geom.store_pace; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -1526,6 +1535,14 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
             c->conv_waves = value;
             return GDP_OK;
+        case GDP_TUNE_STORE_PACE: {
+            if (value < -1 || value > 3) return c->status(GDP_ERR_ARG, "store pace must be -1 (off) or 0..3");
+            const int old = c->geom.store_pace;
+            c->geom.store_pace = value;
+            const int rc = upload_geom(c);
+            if (rc != GDP_OK) c->geom.store_pace = old;
+            return rc;
+        }
         case GDP_TUNE_ZERO_WINDOW: {
             const int old = c->zero_window;
             if (value != 0 && value != 1) return c->status(GDP_ERR_ARG, "zero window must be 0 or 1");

@@ -208,10 +208,11 @@ def test_zero_window_path_is_bit_exact(pkg, oracle, zw):
                 ctx.set_tuning(zero_window=zw)
                 assert ctx.tuning()["zero_window"] == zw
                 ctx.set_input(img)
-                for v in (15, 16, 11, 0, 9, 4):
-                    ctx.set_tuning(variant=v)
+                for v, sp in ((15, -1), (16, 0), (11, 1), (0, 3), (9, -1), (4, 0)):  # sp: GDP_TUNE_STORE_PACE
+                    ctx.set_tuning(variant=v, store_pace=sp)
                     ctx.build()
-                    _assert_same(ctx.pyramid(0), want, ("zero window", zw, H, W, S, O, centre, v))
+                    _assert_same(ctx.pyramid(0), want, ("zero window", zw, H, W, S, O, centre, v, sp))
+                ctx.set_tuning(store_pace=-1)
                 # the in-place window passes on the current contents (re-entry): k_levels, k_levels_x, k_window
                 Oo = O or oracle.default_octaves(H, W)
                 re = want.copy()
