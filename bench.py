@@ -379,7 +379,9 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
             ctxs[0].set_tuning(variant=v)
         except pkg.GdpError:
             break
-        modes = ((0, -1), (0, 1), (1, -1), (1, 0)) if op == "build" else ((0, -1),)
+        # the subset build has no zero window (its levels S..S+2 keep x) but its five stores per group
+        # go out with only two windows' loads between them: pacing alone
+        modes = ((0, -1), (0, 1), (1, -1), (1, 0)) if op == "build" else ((0, -1), (0, 0), (0, 1))
         cands += [(v, o, z, p) for z, p in modes for o in (0, 1)]
     times = {c: [] for c in cands}
     for _ in range(rounds):
@@ -408,16 +410,18 @@ def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
     blocks, or k_levels_x) chosen like the build variant: every candidate timed over the ROTATED
     cold step sequence, interleaved round-robin over `rounds`, median wins.  Bit-identical
     outputs; the best shape depends on the workload (profiles/ab_regen_c*_r02ae.log).  Every shape
-    runs with GDP_TUNE_ZERO_WINDOW off and on (profiles/zwi_*_r03an.log): the pick is a pair."""
+    runs with GDP_TUNE_ZERO_WINDOW off and on (profiles/zwi_*_r03an.log) and, for the re-entry's five
+    stores per thread, paced at vmcnt(1) (GDP_TUNE_STORE_PACE; profiles/spi_regen_c*_r03as.log)."""
     import torch
 
-    cands = [(v, z) for v in values for z in (0, 1)]
+    modes = ((0, -1), (1, -1), (0, 1)) if key == "inplace_sub" else ((0, -1), (1, -1))
+    cands = [(v, z, p) for v in values for z, p in modes]
     times = {cand: [] for cand in cands}
     for _ in range(rounds):
         for cand in cands:
-            v, z = cand
+            v, z, p = cand
             for c in ctxs:
-                c.set_tuning(**{key: v}, zero_window=z)
+                c.set_tuning(**{key: v}, zero_window=z, store_pace=p)
             for f in steps_fn:
                 f(stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -429,7 +433,7 @@ def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
             times[cand].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
     best = min(cands, key=lambda cand: sorted(times[cand])[len(times[cand]) // 2])
     for c in ctxs:
-        c.set_tuning(**{key: best[0]}, zero_window=best[1])
+        c.set_tuning(**{key: best[0]}, zero_window=best[1], store_pace=best[2])
     return best[0]
 
 
@@ -737,7 +741,8 @@ def main():
                     help="with --variant / --inplace-sub: force GDP_TUNE_ZERO_WINDOW too (groups outside every "
                          "window's support skip their window loads; the autotunes otherwise pick it)")
     ap.add_argument("--store-pace", type=int, default=None, choices=[-1, 0, 1, 2, 3],
-                    help="with --variant: force GDP_TUNE_STORE_PACE too (-1 off; n: s_waitcnt vmcnt(n) after each store)")
+                    help="with --variant / --inplace-sub: force GDP_TUNE_STORE_PACE too (-1 off; n: s_waitcnt vmcnt(n) "
+                         "after each store)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
@@ -912,7 +917,7 @@ def main():
             if args.inplace_sub not in values:
                 sys.exit(f"bench.py: --inplace-sub {args.inplace_sub} is not a {key} value ({values})")
             for c in ctxs:
-                c.set_tuning(**{key: args.inplace_sub}, zero_window=args.zero_window)
+                c.set_tuning(**{key: args.inplace_sub}, zero_window=args.zero_window, store_pace=args.store_pace)
         elif not args.no_autotune:
             autotuned = (key, autotune_inplace(ctxs, steps_fn, stream, 3 if B * H * W > (1 << 28) else 10, key, values))
     n_step = [0]
@@ -1027,11 +1032,14 @@ def main():
                           " (autotuned)" if autotuned else "")
                        if args.op == "build" else
                        "k_build<SUB> (fused decimate+window+DoG, GenerateDoG_nomp_dynamic's subset of levels), "
-                       "variant %d, tile order %d" % (ctx.tuning()["variant"], ctx.tuning()["tile_order"])
+                       "variant %d, tile order %d, store pace %s" % (tun["variant"], tun["tile_order"],
+                                                                     "off" if tun["store_pace"] < 0 else
+                                                                     "vmcnt(%d)" % tun["store_pace"])
                        if args.op == "subset" else
                        {"regen": ("k_levels_x (in-place window+DoG, one level per wave)" if tun["inplace_sub"] == 0 else
                                   "k_levels<MODE=3> (in-place window+DoG, all octaves, %d-thread blocks)"
-                                  % (1024 // tun["inplace_sub"])) + ", zero window %d" % tun["zero_window"]
+                                  % (1024 // tun["inplace_sub"])) + ", zero window %d, store pace %s" % (
+                                     tun["zero_window"], "off" if tun["store_pace"] < 0 else "vmcnt(%d)" % tun["store_pace"])
                                  + (" (autotuned)" if autotuned else ""),
                         "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks), zero window %d%s"
                                  % (1024 // tun["window_sub"], tun["zero_window"], " (autotuned)" if autotuned else ""),
