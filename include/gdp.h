@@ -296,14 +296,17 @@ enum {
                                    in-place window passes (gdp_generate_dog, gdp_gauss_*) form
                                    v * 0.0f.  The same bits either way; 0 (default) off */
     GDP_TUNE_STORE_PACE = 17    /* -1 (default) off; n = 0..3: after each pyramid store of the
-                                   convolution block tiles and of the build's outside-support
-                                   groups, wait until at most n memory operations of the wave are
-                                   outstanding (A/B knob; the same bits either way) */
+                                   build (full, subset and outside-support paths), the in-place
+                                   re-entry and the convolution block tiles, wait until at most n
+                                   memory operations of the wave are outstanding (s_waitcnt
+                                   vmcnt(n)); the same bits either way */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
-/* Benchmark every build-kernel variant x tile order on the context's current input (`iters`
- * launches each, HIP events on `stream`) and keep the fastest; reports the choice and its
- * per-launch ms.  Results are bit-identical for every candidate.  Overwrites the pyramid. */
+/* Benchmark every build-kernel variant x tile order x store mode (GDP_TUNE_ZERO_WINDOW,
+ * GDP_TUNE_STORE_PACE) in (0, off) (0, 1) (1, off) (1, 0) on the context's current input (`iters`
+ * launches each, HIP events on `stream`) and keep the fastest; reports the variant, tile order
+ * (the store mode: gdp_get_tuning) and its per-launch ms.  Results are bit-identical for every
+ * candidate.  Overwrites the pyramid. */
 int gdp_autotune(gdp_ctx* ctx, int iters, void* stream, int* variant, int* tile_order, float* ms_per_build);
 int gdp_get_tuning(const gdp_ctx* ctx, int key, int* value);
 

@@ -286,7 +286,8 @@ void set_window_support(gdp_ctx* c, bool on) {
         og.nz_c1 = og.cols;
         if (!on) continue;
         auto support = [&](int length, int& lo, int& hi) {
-            std::vector<float> t((size_t)std::max(1, length >> o));
+            // host_taps writes (int) of the float-halved length: above 2^24 that can round up
+            std::vector<float> t((size_t)std::max(1, length >> o) + 8);
             lo = INT32_MAX;
             hi = 0;
             for (int mode : {GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN})

@@ -273,7 +273,8 @@ class PyramidContext:
                 check(lib().gdp_set_tuning(self._ctx, self._tuning_key(name), int(vals[name])), self._ctx)
 
     def autotune(self, iters=5, stream=None):
-        """Time every build variant x tile order on the current input and keep the fastest;
+        """Time every build variant x tile order x store mode (zero_window, store_pace) on the
+        current input and keep the fastest;
         returns (variant, tile_order, ms per build).  Overwrites the pyramid (bits unchanged)."""
         v, o, ms = _i(), _i(), ctypes.c_float()
         check(lib().gdp_autotune(self._ctx, int(iters), _stream_handle(stream), ctypes.byref(v), ctypes.byref(o),
