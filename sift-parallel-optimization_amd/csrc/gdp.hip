@@ -29,6 +29,7 @@
 #include <thread>
 #include <type_traits>
 #include <utility>
+#include <array>
 #include <vector>
 
 #include "gdp.h"
@@ -97,6 +98,7 @@ struct gdp_ctx {
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
     int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
+    std::vector<std::array<int, 4>> support; // per octave: nz_r0, nz_r1, nz_c0, nz_c1 (set_window_support)
     int zero_window = 0;          // GDP_TUNE_ZERO_WINDOW: build groups outside the windows' support store
                                   // their input-independent levels without waiting for the input
     int conv_order = 4;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
@@ -275,34 +277,42 @@ void fill_host_taps(gdp_ctx* c, int mode) {
 // table pointer swap, needs no geometry change).  The reference's windows underflow to +0 a few
 // σ from the centre (expf(-d²/(2σ²)) = 0 for d >= 29 at σ = 2), so on a large image almost every
 // pixel lies outside them.  `on` = 0: the ranges cover the whole octave (every group computed).
+// The ranges are computed once per context (host expf over every row and column of every octave)
+// and only copied in and out of the Geom when the knob changes.
 void set_window_support(gdp_ctx* c, bool on) {
     Geom& g = c->geom;
+    if (on && c->support.size() != (size_t)g.O) {
+        c->support.assign((size_t)g.O, {0, 0, 0, 0});
+        for (int o = 0; o < g.O; ++o) {
+            auto support = [&](int length, int& lo, int& hi) {
+                // host_taps writes (int) of the float-halved length: above 2^24 that can round up
+                std::vector<float> t((size_t)std::max(1, length >> o) + 8);
+                lo = INT32_MAX;
+                hi = 0;
+                for (int mode : {GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN})
+                    for (int s = 0; s < g.L; ++s) {
+                        const int n = host_taps(length, o, s, t.data(), mode);
+                        for (int i = 0; i < n; ++i)
+                            if (t[i] != 0.0f) {
+                                lo = std::min(lo, i);
+                                hi = std::max(hi, i + 1);
+                            }
+                    }
+                if (lo > hi) lo = hi = 0; // no non-zero tap at all: every pixel is outside
+            };
+            auto& r = c->support[(size_t)o];
+            support(g.W, r[2], r[3]);
+            support(g.H, r[0], r[1]);
+        }
+    }
     for (int o = 0; o < g.O; ++o) {
         OctGeom& og = g.oct[o];
-        const int Hg = g.H >> o;
-        og.nz_r0 = 0;
-        og.nz_r1 = Hg;
-        og.nz_c0 = 0;
-        og.nz_c1 = og.cols;
-        if (!on) continue;
-        auto support = [&](int length, int& lo, int& hi) {
-            // host_taps writes (int) of the float-halved length: above 2^24 that can round up
-            std::vector<float> t((size_t)std::max(1, length >> o) + 8);
-            lo = INT32_MAX;
-            hi = 0;
-            for (int mode : {GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN})
-                for (int s = 0; s < g.L; ++s) {
-                    const int n = host_taps(length, o, s, t.data(), mode);
-                    for (int i = 0; i < n; ++i)
-                        if (t[i] != 0.0f) {
-                            lo = std::min(lo, i);
-                            hi = std::max(hi, i + 1);
-                        }
-                }
-            if (lo > hi) lo = hi = 0; // no non-zero tap at all: every pixel is outside
-        };
-        support(g.W, og.nz_c0, og.nz_c1);
-        support(g.H, og.nz_r0, og.nz_r1);
+        if (on) {
+            const auto& r = c->support[(size_t)o];
+            og.nz_r0 = r[0], og.nz_r1 = r[1], og.nz_c0 = r[2], og.nz_c1 = r[3];
+        } else {
+            og.nz_r0 = 0, og.nz_r1 = g.H >> o, og.nz_c0 = 0, og.nz_c1 = og.cols;
+        }
     }
 }
 
