@@ -1044,8 +1044,9 @@ def main():
                         "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks), zero window %d%s"
                                  % (1024 // tun["window_sub"], tun["zero_window"], " (autotuned)" if autotuned else ""),
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
-                                 "240-column block tiles on %d waves, DPP lane shifts)"
-                                 % (ctx.tuning()["conv_rows"], ctx.tuning().get("conv_waves") or 16)
+                                 "240-column block tiles on %d waves, DPP lane shifts, store pace %s)"
+                                 % (ctx.tuning()["conv_rows"], ctx.tuning().get("conv_waves") or 16,
+                                    "off" if tun["conv_pace"] < 0 else "vmcnt(%d)" % tun["conv_pace"])
                                  if ctx.tuning()["conv_kernel"] == 2 and S <= 5 else
                                  "k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
                                  "DPP lane shifts, %d-row strips)" % ctx.tuning()["conv_rows"]

@@ -295,11 +295,11 @@ enum {
                                    before the input lands and level S+2 as copysign(0, x); the
                                    in-place window passes (gdp_generate_dog, gdp_gauss_*) form
                                    v * 0.0f.  The same bits either way; 0 (default) off */
-    GDP_TUNE_STORE_PACE = 17    /* -1 (default) off; n = 0..3: after each pyramid store of the
-                                   build (full, subset and outside-support paths), the in-place
-                                   re-entry and the convolution block tiles, wait until at most n
-                                   memory operations of the wave are outstanding (s_waitcnt
-                                   vmcnt(n)); the same bits either way */
+    GDP_TUNE_STORE_PACE = 17,   /* -1 (default) off; n = 0..3: after each pyramid store of the
+                                   build (full, subset and outside-support paths) and the in-place
+                                   re-entry, wait until at most n memory operations of the wave
+                                   are outstanding (s_waitcnt vmcnt(n)); the same bits either way */
+    GDP_TUNE_CONV_PACE = 18     /* the same for gdp_build_gaussian's block tiles (default 2) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order x store mode (GDP_TUNE_ZERO_WINDOW,

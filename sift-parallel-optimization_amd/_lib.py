@@ -27,6 +27,7 @@ GDP_TUNE_CONV_ORDER, GDP_TUNE_BUILD_LDS, GDP_TUNE_STAGE_KB, GDP_TUNE_STAGE_THREA
 GDP_TUNE_CONV_WAVES = 15
 GDP_TUNE_ZERO_WINDOW = 16
 GDP_TUNE_STORE_PACE = 17
+GDP_TUNE_CONV_PACE = 18
 
 
 class GdpError(RuntimeError):

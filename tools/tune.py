@@ -66,6 +66,7 @@ def main():
             del variants[-1][1]["variant"]
         variants[-1][1]["zero_window"] = int(kv.get("zw", 0))  # every variant sets it (apply() keeps state)
         variants[-1][1]["store_pace"] = int(kv.get("sp", -1))
+        variants[-1][1]["conv_pace"] = int(kv.get("cp", 2))
         if "bpc" in kv:
             variants[-1][1]["blocks_per_cu"] = int(kv["bpc"])
         if "ip" in kv or "is" in kv:  # timing-only: read a caller buffer with this input pitch / image stride
