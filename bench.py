@@ -758,7 +758,7 @@ def main():
     ap.add_argument("--conv-kernel", type=int, default=None,
                     help="--op conv: 0 register sweep, 1 LDS tiles, 2 block tiles (default)")
     ap.add_argument("--conv-rows", type=int, default=None,
-                    help="--op conv: block tiles' rows per block (32 default) / the sweep's rows per strip (16/32)")
+                    help="--op conv: block tiles' rows per block (48 default) / the sweep's rows per strip (16/32)")
     ap.add_argument("--conv-order", type=int, default=None,
                     help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
                          "after their input rows; default 4)")

@@ -275,8 +275,8 @@ enum {
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default; 1, 2, 8, 16) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (S <= 3), 1 LDS tiles,
                                    2 block tiles (default; one output row per wave, S <= 5) */
-    GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian: block tiles' rows per block (32 default;
-                                   16 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8); the sweep's
+    GDP_TUNE_CONV_ROWS = 9,     /* gdp_build_gaussian: block tiles' rows per block (48 default;
+                                   16 / 32 with 16 waves, 8 / 16 / 24 / 32 with 8); the sweep's
                                    rows per wave strip (16 / 32) */
     GDP_TUNE_CONV_ORDER = 11,   /* gdp_build_gaussian block order: bit 0 XCD-chunked, bit 1 odd
                                    sweep waves go bottom-up (sweep only), bit 2 (default 4) octave

@@ -96,7 +96,7 @@ struct gdp_ctx {
     float* d_taps_mode[2] = {nullptr, nullptr}; // one device tap table per window-centre mode, built on
                                   // first use, so switching centres is a pointer swap (no drain)
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
-    int conv_rows = 32;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
+    int conv_rows = 48;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
     std::vector<std::array<int, 4>> support; // per octave: nz_r0, nz_r1, nz_c0, nz_c1 (set_window_support)
     int zero_window = 0;          // GDP_TUNE_ZERO_WINDOW: build groups outside the windows' support store
@@ -528,12 +528,15 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // single images (4096^2 0.148 vs 0.152 ms for 256 threads, 16384^2 2.37 vs 2.49;
     // profiles/ab_sub_c*_r03m.log), 256-thread blocks on small batches, 1024-thread above
     c->inplace_sub = batch == 1 ? 16 : (long long)(row_end - row_begin) * W * batch <= (32ll << 20) ? 4 : 1;
-    // Convolution extension default: block tiles of 32 rows (16 waves) in block order 4 (octave-o
-    // block rows right after the octave-0 rows that hold their input rows, no XCD chunking) —
-    // the fastest form on every config (tools/conv_ab.sh, cold buffers: 4096^2 0.111 ms vs 0.119
-    // for the sweep, 64 x 1080x1920 0.795 vs 0.809, 64 x 4096^2 6.34 vs 6.79, 16384^2 1.62 vs 1.72).
+    // Convolution extension default: block tiles (16 waves) in block order 4 (octave-o block rows
+    // right after the octave-0 rows that hold their input rows, no XCD chunking) — the fastest form
+    // on every config (tools/conv_ab.sh, cold buffers: 4096^2 0.111 ms vs 0.119 for the sweep,
+    // 64 x 1080x1920 0.795 vs 0.809, 64 x 4096^2 6.34 vs 6.79, 16384^2 1.62 vs 1.72).  48 rows per
+    // block since round 3: unpaced, 48 and 32 rows ran equal; with the stores paced at vmcnt(2)
+    // (GDP_TUNE_CONV_PACE) 48 rows is 2-3 % ahead of 32 on every config (4096^2 0.1031 vs 0.1056 ms,
+    // 64 x 4096^2 5.72 vs 5.92, 16384^2 1.461 vs 1.509; profiles/cpw_conv_c*_r03aw.log).
     c->conv_kernel = 2;
-    c->conv_rows = 32;
+    c->conv_rows = 48;
     c->conv_order = 4;
     {
         const unsigned hw = std::thread::hardware_concurrency();

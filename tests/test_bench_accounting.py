@@ -220,6 +220,9 @@ def test_traffic_records_match_only_their_kernel_instance():
     assert bench.latest_pmc("c2", 99, 0) is None
     conv = bench.latest_conv_pmc("c2", {"conv_kernel": 2, "conv_rows": 32, "conv_order": 4})
     assert conv is not None and conv["op"] == "conv"
+    for cfg in ("c2", "c4", "c5"):  # the round-3 default: 48-row block tiles
+        rec = bench.latest_conv_pmc(cfg, {"conv_kernel": 2, "conv_rows": 48, "conv_order": 4})
+        assert rec is not None and "k_conv_blk<5, 48, 16>" in rec["kernel"], cfg
     assert bench.latest_conv_pmc("c2", {"conv_kernel": 0, "conv_rows": 16, "conv_order": 0}) is None
 
 
