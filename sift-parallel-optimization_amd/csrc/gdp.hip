@@ -333,7 +333,9 @@ static int conv_sweep_rows(const gdp_ctx* c) { return c->conv_rows == 32 ? 32 : 
 // (Measured and dropped, round 3: 64-row tiles on 16 waves — 80 staged rows, 80 KB of LDS, two
 // blocks per CU — cut the staged-row overhead from 44/32 to 76/64 but ran slower on every config:
 // 4096^2 0.110 vs 0.099 ms, 64 x 1080 x 1920 0.767 vs 0.714, 64 x 4096^2 5.95 vs 5.71, 16384^2
-// 1.48 vs 1.45; profiles/conv_ab_r03c.log.)
+// 1.48 vs 1.45; profiles/conv_ab_r03c.log.  Re-measured with the stores paced, still behind the
+// 48-row default: 4096^2 0.1088 vs 0.1021 ms, 64 x 4096^2 5.84 vs 5.69, 16384^2 1.483 vs 1.453;
+// profiles/cpy_conv_c*_r03ay.log.)
 static bool conv_blk_pair_ok(int rows, int waves) {
     return waves == 16 ? (rows == 16 || rows == 32 || rows == 48)
                        : waves == 8 && (rows == 8 || rows == 16 || rows == 24 || rows == 32);
