@@ -421,7 +421,7 @@ def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
         for cand in cands:
             v, z, p = cand
             for c in ctxs:
-                c.set_tuning(**{key: v}, zero_window=z, store_pace=p)
+                c.set_tuning(**{key: v}, zero_window=z, inplace_pace=p)
             for f in steps_fn:
                 f(stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -433,7 +433,7 @@ def autotune_inplace(ctxs, steps_fn, stream, iters, key, values, rounds=5):
             times[cand].append(e0.elapsed_time(e1) / (iters * len(ctxs)))
     best = min(cands, key=lambda cand: sorted(times[cand])[len(times[cand]) // 2])
     for c in ctxs:
-        c.set_tuning(**{key: best[0]}, zero_window=best[1], store_pace=best[2])
+        c.set_tuning(**{key: best[0]}, zero_window=best[1], inplace_pace=best[2])
     return best[0]
 
 
@@ -917,7 +917,7 @@ def main():
             if args.inplace_sub not in values:
                 sys.exit(f"bench.py: --inplace-sub {args.inplace_sub} is not a {key} value ({values})")
             for c in ctxs:
-                c.set_tuning(**{key: args.inplace_sub}, zero_window=args.zero_window, store_pace=args.store_pace)
+                c.set_tuning(**{key: args.inplace_sub}, zero_window=args.zero_window, inplace_pace=args.store_pace)
         elif not args.no_autotune:
             autotuned = (key, autotune_inplace(ctxs, steps_fn, stream, 3 if B * H * W > (1 << 28) else 10, key, values))
     n_step = [0]
@@ -1039,7 +1039,7 @@ def main():
                        {"regen": ("k_levels_x (in-place window+DoG, one level per wave)" if tun["inplace_sub"] == 0 else
                                   "k_levels<MODE=3> (in-place window+DoG, all octaves, %d-thread blocks)"
                                   % (1024 // tun["inplace_sub"])) + ", zero window %d, store pace %s" % (
-                                     tun["zero_window"], "off" if tun["store_pace"] < 0 else "vmcnt(%d)" % tun["store_pace"])
+                                     tun["zero_window"], "off" if tun["inplace_pace"] < 0 else "vmcnt(%d)" % tun["inplace_pace"])
                                  + (" (autotuned)" if autotuned else ""),
                         "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks), zero window %d%s"
                                  % (1024 // tun["window_sub"], tun["zero_window"], " (autotuned)" if autotuned else ""),

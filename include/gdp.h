@@ -199,6 +199,25 @@ int gdp_download_level_range(gdp_ctx* ctx, int b, int octave, int scale, int fir
 int gdp_download_pyramid(gdp_ctx* ctx, int b, float* host);
 /* Upload a packed pyramid of image b (state restore; used by re-entry tests). */
 int gdp_upload_pyramid(gdp_ctx* ctx, int b, const float* host);
+/* Host -> device state: the reference's float**** GaussPy IS its pyramid, and GaussFilter /
+ * GenerateDoG work on whatever the caller left in it (GuassDePyramid.h:16, :122-131, :140-146).
+ * These copy a caller-edited host pyramid back into the device levels (blocking), so an in-place
+ * call that follows processes the caller's edits.  The drop-in classes call them before every
+ * mutating method when `mirror_host` is set or the caller flagged `host_dirty`
+ * (include/GaussDePyramid-HIP.h).
+ *   gdp_upload_level:        level (o, s) of image b from a dense rows x cols host array
+ *   gdp_upload_level_rows:   the same from host row pointers (GaussPy[o][s])
+ *   gdp_upload_pyramid_rows: every level of image b from GaussPy[o][s][row] (the inverse of
+ *                            gdp_download_pyramid_rows; rows gathered through the double-buffered
+ *                            pinned staging, the H2D copy of one batch overlapping the gather of
+ *                            the next)
+ *   gdp_upload_image_raw:    image b's pyramid in the device layout (gdp_image_floats floats,
+ *                            level (o, s) at gdp_level_offset(ctx, 0, o, s)) in ONE H2D copy — the
+ *                            inverse of gdp_download_image_raw */
+int gdp_upload_level(gdp_ctx* ctx, int b, int octave, int scale, const float* host);
+int gdp_upload_level_rows(gdp_ctx* ctx, int b, int octave, int scale, const float* const* rows);
+int gdp_upload_pyramid_rows(gdp_ctx* ctx, int b, const float* const* const* const* gauss_py);
+int gdp_upload_image_raw(gdp_ctx* ctx, int b, const float* host);
 /* Float elements of one image's packed pyramid (what gdp_download_pyramid writes). */
 size_t gdp_packed_floats(const gdp_ctx* ctx);
 /* Zero-copy output: write the pyramids into caller-owned DEVICE memory of at least
@@ -296,17 +315,22 @@ enum {
                                    in-place window passes (gdp_generate_dog, gdp_gauss_*) form
                                    v * 0.0f.  The same bits either way; 0 (default) off */
     GDP_TUNE_STORE_PACE = 17,   /* -1 (default) off; n = 0..3: after each pyramid store of the
-                                   build (full, subset and outside-support paths) and the in-place
-                                   re-entry, wait until at most n memory operations of the wave
-                                   are outstanding (s_waitcnt vmcnt(n)); the same bits either way */
-    GDP_TUNE_CONV_PACE = 18     /* the same for gdp_build_gaussian's block tiles (default 2) */
+                                   build (full, subset and outside-support paths), wait until at
+                                   most n memory operations of the wave are outstanding
+                                   (s_waitcnt vmcnt(n)); the same bits either way */
+    GDP_TUNE_CONV_PACE = 18,    /* the same for gdp_build_gaussian's block tiles (default 2) */
+    GDP_TUNE_INPLACE_PACE = 19  /* the same for the in-place re-entry (gdp_generate_dog, k_levels;
+                                   default -1): its own field, so tuning the build's pacing never
+                                   changes the in-place passes' speed */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order x store mode (GDP_TUNE_ZERO_WINDOW,
  * GDP_TUNE_STORE_PACE) in (0, off) (0, 1) (1, off) (1, 0) on the context's current input (`iters`
  * launches each, HIP events on `stream`) and keep the fastest; reports the variant, tile order
  * (the store mode: gdp_get_tuning) and its per-launch ms.  Results are bit-identical for every
- * candidate.  Overwrites the pyramid. */
+ * candidate.  Overwrites the pyramid.  NB: GDP_TUNE_ZERO_WINDOW is context-wide — the pick also
+ * applies to the in-place window passes that run later on this context (bit-identical either
+ * way); GDP_TUNE_STORE_PACE applies to the builds only (the re-entry has GDP_TUNE_INPLACE_PACE). */
 int gdp_autotune(gdp_ctx* ctx, int iters, void* stream, int* variant, int* tile_order, float* ms_per_build);
 int gdp_get_tuning(const gdp_ctx* ctx, int key, int* value);
 

@@ -28,6 +28,7 @@ GDP_TUNE_CONV_WAVES = 15
 GDP_TUNE_ZERO_WINDOW = 16
 GDP_TUNE_STORE_PACE = 17
 GDP_TUNE_CONV_PACE = 18
+GDP_TUNE_INPLACE_PACE = 19
 
 
 class GdpError(RuntimeError):
@@ -84,6 +85,10 @@ SIGNATURES = {
     "gdp_download_pyramid_rows": (_c_int, [_p, _c_int, _p]),
     "gdp_download_pyramid": (_c_int, [_p, _c_int, _p]),
     "gdp_upload_pyramid": (_c_int, [_p, _c_int, _p]),
+    "gdp_upload_level": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_upload_level_rows": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
+    "gdp_upload_pyramid_rows": (_c_int, [_p, _c_int, _p]),
+    "gdp_upload_image_raw": (_c_int, [_p, _c_int, _p]),
     "gdp_packed_floats": (_c_size, [_p]),
     "gdp_set_output_device": (_c_int, [_p, _p, _c_size]),
     "gdp_level_offset": (_c_size, [_p, _c_int, _c_int, _c_int]),

@@ -98,7 +98,9 @@ struct gdp_ctx {
     int conv_kernel = 2;          // GDP_TUNE_CONV_KERNEL: 0 register sweep, 1 LDS tiles, 2 block tiles (default)
     int conv_rows = 48;           // GDP_TUNE_CONV_ROWS: output rows per wave strip of the sweep / per block tile
     int conv_waves = 16;          // GDP_TUNE_CONV_WAVES: waves per block of the block tiles
-    std::vector<std::array<int, 4>> support; // per octave: nz_r0, nz_r1, nz_c0, nz_c1 (set_window_support)
+    bool conv_rows_set = false;   // GDP_TUNE_CONV_ROWS set by the caller; until then the rows follow
+                                  // the selected kernel / waves (conv_default_rows)
+    std::vector<std::array<int, 5>> support; // per octave: nz_r0, nz_r1, nz_c0, nz_c1, rows exact in place
     int zero_window = 0;          // GDP_TUNE_ZERO_WINDOW: build groups outside the windows' support store
                                   // their input-independent levels without waiting for the input
     int conv_order = 4;           // GDP_TUNE_CONV_ORDER: bit 0 XCD-chunked blocks, bit 1 alternate sweep directions,
@@ -259,15 +261,26 @@ void fill_host_taps(gdp_ctx* c, int mode) {
     const Geom& g = c->geom;
     for (int o = 0; o < g.O; ++o) {
         const OctGeom& og = g.oct[o];
-        std::vector<float> rows(og.rtap_row == 1 ? 0 : (size_t)(g.H >> o));
+        // host_taps writes (int) of the float-halved axis length, which above 2^24 can round to one
+        // more (or fewer) than len >> o: compute into scratch sized with slack and copy exactly the
+        // len >> o taps the octave has (taps the float length did not reach stay +0)
+        const int Hg = g.H >> o, Wg = og.cols;
+        std::vector<float> t((size_t)std::max(1, std::max(Hg, Wg)) + 8);
+        auto taps_of = [&](int length, int n_axis, int s) {
+            std::fill(t.begin(), t.end(), 0.0f);
+            host_taps(length, o, s, t.data(), mode);
+            return n_axis;
+        };
         for (int s = 0; s < g.L; ++s) {
-            host_taps(g.W, o, s, c->h_taps.data() + og.ctap + (long long)s * og.ctap_stride, mode);
+            const int nc = taps_of(g.W, Wg, s);
+            std::copy(t.begin(), t.begin() + nc, c->h_taps.begin() + og.ctap + (long long)s * og.ctap_stride);
             if (og.rtap_row == 1) {  // contiguous per scale (a square image's: the column taps again)
-                host_taps(g.H, o, s, c->h_taps.data() + og.rtap + (long long)s * og.rtap_stride, mode);
+                const int nr = taps_of(g.H, Hg, s);
+                std::copy(t.begin(), t.begin() + nr, c->h_taps.begin() + og.rtap + (long long)s * og.rtap_stride);
                 continue;
             }
-            const int n = host_taps(g.H, o, s, rows.data(), mode);  // [row][scale] interleaved
-            for (int r = 0; r < n; ++r) c->h_taps[og.rtap + (size_t)r * og.rtap_row + s] = rows[r];
+            const int nr = taps_of(g.H, Hg, s);  // [row][scale] interleaved
+            for (int r = 0; r < nr; ++r) c->h_taps[og.rtap + (size_t)r * og.rtap_row + s] = t[r];
         }
     }
 }
@@ -282,27 +295,32 @@ void fill_host_taps(gdp_ctx* c, int mode) {
 void set_window_support(gdp_ctx* c, bool on) {
     Geom& g = c->geom;
     if (on && c->support.size() != (size_t)g.O) {
-        c->support.assign((size_t)g.O, {0, 0, 0, 0});
+        c->support.assign((size_t)g.O, {0, 0, 0, 0, 0});
         for (int o = 0; o < g.O; ++o) {
-            auto support = [&](int length, int& lo, int& hi) {
+            auto support = [&](int length, int& lo, int& hi, float& peak) {
                 // host_taps writes (int) of the float-halved length: above 2^24 that can round up
                 std::vector<float> t((size_t)std::max(1, length >> o) + 8);
                 lo = INT32_MAX;
                 hi = 0;
+                peak = 0.0f;
                 for (int mode : {GDP_CENTRE_SERIAL, GDP_CENTRE_INTLEN})
                     for (int s = 0; s < g.L; ++s) {
-                        const int n = host_taps(length, o, s, t.data(), mode);
-                        for (int i = 0; i < n; ++i)
+                        const int n = std::min(host_taps(length, o, s, t.data(), mode), std::max(0, length >> o));
+                        for (int i = 0; i < n; ++i) {
+                            peak = std::max(peak, t[i]);
                             if (t[i] != 0.0f) {
                                 lo = std::min(lo, i);
                                 hi = std::max(hi, i + 1);
                             }
+                        }
                     }
                 if (lo > hi) lo = hi = 0; // no non-zero tap at all: every pixel is outside
             };
             auto& r = c->support[(size_t)o];
-            support(g.W, r[2], r[3]);
-            support(g.H, r[0], r[1]);
+            float col_peak = 0.0f, row_peak = 0.0f;
+            support(g.W, r[2], r[3], col_peak);
+            support(g.H, r[0], r[1], row_peak);
+            r[4] = col_peak <= 1.0f ? 1 : 0;  // rows outside the support exact for the in-place passes
         }
     }
     for (int o = 0; o < g.O; ++o) {
@@ -310,8 +328,10 @@ void set_window_support(gdp_ctx* c, bool on) {
         if (on) {
             const auto& r = c->support[(size_t)o];
             og.nz_r0 = r[0], og.nz_r1 = r[1], og.nz_c0 = r[2], og.nz_c1 = r[3];
+            og.nzi_r0 = r[4] ? r[0] : 0;
+            og.nzi_r1 = r[4] ? r[1] : g.H >> o;
         } else {
-            og.nz_r0 = 0, og.nz_r1 = g.H >> o, og.nz_c0 = 0, og.nz_c1 = og.cols;
+            og.nz_r0 = og.nzi_r0 = 0, og.nz_r1 = og.nzi_r1 = g.H >> o, og.nz_c0 = 0, og.nz_c1 = og.cols;
         }
     }
 }
@@ -340,6 +360,14 @@ static bool conv_blk_pair_ok(int rows, int waves) {
     return waves == 16 ? (rows == 16 || rows == 32 || rows == 48)
                        : waves == 8 && (rows == 8 || rows == 16 || rows == 24 || rows == 32);
 }
+// Rows per tile / strip when the caller has not chosen them: the sweep's 16-row strips, the block
+// tiles' 48 rows on 16 waves (the default) and 32 on 8 waves — so selecting only the kernel or only
+// the waves never leaves an uninstantiated pair.  The LDS tiles take no row count.
+static int conv_default_rows(const gdp_ctx* c) {
+    if (c->conv_kernel == 0) return 16;
+    if (c->conv_kernel == 2) return c->conv_waves == 8 ? 32 : 48;
+    return c->conv_rows;
+}
 static void conv_sweep_geom(gdp_ctx* c) {
     Geom& g = c->geom;
     const int strip_cols = SwGeom<kSwV>::kCols;
@@ -358,6 +386,21 @@ static void conv_sweep_geom(gdp_ctx* c) {
     }
     c->conv_perm_dirty = true;
 }
+
+static int conv_set_rows(gdp_ctx* c, int rows) {
+    if (rows == c->conv_rows) return GDP_OK;
+    const int old = c->conv_rows;
+    c->conv_rows = rows;
+    conv_sweep_geom(c);
+    const int rc = upload_geom(c);
+    if (rc != GDP_OK) {
+        c->conv_rows = old;
+        conv_sweep_geom(c);
+    }
+    return rc;
+}
+// after a kernel / waves change: rows the caller never set follow the selection
+static int conv_follow_rows(gdp_ctx* c) { return c->conv_rows_set ? GDP_OK : conv_set_rows(c, conv_default_rows(c)); }
 
 // Input-row-interleaved block order of the convolution sweep / block tiles (GDP_TUNE_CONV_ORDER
 // bit 2): each octave-o block row (2^o times as many input rows as an octave-0 block row) is
@@ -558,6 +601,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     g.in_img_stride = (long long)g.in_rows * g.in_pitch;
     g.vec_in = 1;
     g.store_pace = -1;
+    g.inplace_pace = -1;
     // the convolution block tiles' five stores per output row go out back to back; vmcnt(2) after
     // each measured 0.5-1.3 % faster on 4096^2 / 64 x 4096^2 / 16384^2 (profiles/sp_conv_c*_r03ap.log)
     g.conv_pace = 2;
@@ -1299,6 +1343,121 @@ int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) try {
     return GDP_OK;
 } GDP_ABI_CATCH(c)
 
+// ---- host -> device state (the drop-in classes' two-way GaussPy, GuassDePyramid.h:16) ----------
+// The reference's float**** IS the pyramid: GaussFilter / GenerateDoG work on whatever the caller
+// left in it (:122-131, :140-146).  These copy a host-side pyramid back into the device levels.
+// Staged row uploads are the mirror of stage_download: the host threads gather batch k into one
+// pinned half while batch k-1's H2D copy runs out of the other.
+struct UpPiece {
+    float* dst;                 // device rows [0, nrows) of a level slice, `cols` floats each
+    size_t cols, nrows;
+    const float* const* rows;   // the caller's source row pointers for those rows
+};
+
+static int stage_upload(gdp_ctx* c, const std::vector<UpPiece>& pieces) {
+    size_t total = 0, max_cols = 1;
+    for (const UpPiece& q : pieces) {
+        total += q.cols * q.nrows;
+        max_cols = std::max(max_cols, q.cols);
+        for (size_t r = 0; r < q.nrows; ++r)
+            if (!q.rows[r]) return c->status(GDP_ERR_ARG, "pyramid row upload: null row pointer");
+    }
+    if (total == 0) return GDP_OK;
+    size_t half = std::max(c->stage_half_floats, max_cols);
+    const bool dbl = total > half;
+    if (!dbl) half = total;
+    const int rc = ensure_stage(c, dbl ? 2 * half : half);
+    if (rc != GDP_OK) return rc;
+    struct Cut { const UpPiece* q; size_t r0, nr, off; };
+    std::vector<std::vector<Cut>> batches(1);
+    std::vector<size_t> used(1, 0);
+    for (const UpPiece& q : pieces)
+        for (size_t r = 0; r < q.nrows;) {
+            size_t fit = (half - used.back()) / q.cols;
+            if (fit == 0) {
+                batches.emplace_back();
+                used.push_back(0);
+                fit = half / q.cols;
+            }
+            const size_t nr = std::min(fit, q.nrows - r);
+            batches.back().push_back({&q, r, nr, used.back()});
+            used.back() += nr * q.cols;
+            r += nr;
+        }
+    for (size_t k = 0; k < batches.size(); ++k) {
+        float* h = c->h_stage + (k & 1) * half;
+        if (k >= 2) GDP_HIP(c, hipEventSynchronize(c->ev_stage[k & 1]));  // batch k-2 has left this half
+        const std::vector<Cut>& bk = batches[k];
+        size_t rows = 0;
+        for (const Cut& t : bk) rows = std::max(rows, t.nr);
+        parallel_rows(rows, used[k], c->stage_threads, [&](size_t a, size_t e) {
+            for (const Cut& t : bk) {
+                const size_t r0 = t.nr * a / rows, r1 = t.nr * e / rows;
+                for (size_t r = r0; r < r1; ++r)
+                    std::memcpy(h + t.off + r * t.q->cols, t.q->rows[t.r0 + r], t.q->cols * 4);
+            }
+        });
+        for (size_t i = 0; i < bk.size();) {  // device-adjacent slices go as one copy
+            size_t n = bk[i].nr * bk[i].q->cols, j = i + 1;
+            float* dst = bk[i].q->dst + bk[i].r0 * bk[i].q->cols;
+            for (; j < bk.size() && bk[j].q->dst + bk[j].r0 * bk[j].q->cols == dst + n && bk[j].off == bk[i].off + n; ++j)
+                n += bk[j].nr * bk[j].q->cols;
+            GDP_HIP(c, hipMemcpyAsync(dst, h + bk[i].off, n * 4, hipMemcpyHostToDevice, c->stream));
+            i = j;
+        }
+        GDP_HIP(c, hipEventRecord(c->ev_stage[k & 1], c->stream));
+    }
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+}
+
+int gdp_upload_level(gdp_ctx* c, int b, int o, int s, const float* host) try {
+    if (!valid_level(c, b, o, s) || !host) return c ? c->status(GDP_ERR_ARG, "gdp_upload_level: bad argument") : GDP_ERR_ARG;
+    const OctGeom& og = c->geom.oct[o];
+    if ((size_t)og.rows * og.cols == 0) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), host, (size_t)og.rows * og.cols * 4,
+                              hipMemcpyHostToDevice, c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+int gdp_upload_level_rows(gdp_ctx* c, int b, int o, int s, const float* const* rows) try {
+    if (!valid_level(c, b, o, s) || !rows) return c ? c->status(GDP_ERR_ARG, "gdp_upload_level_rows: bad argument") : GDP_ERR_ARG;
+    const OctGeom& og = c->geom.oct[o];
+    if ((size_t)og.rows * og.cols == 0) return GDP_OK;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return stage_upload(c, {{const_cast<float*>(gdp_device_level(c, b, o, s)), (size_t)og.cols, (size_t)og.rows, rows}});
+} GDP_ABI_CATCH(c)
+
+int gdp_upload_pyramid_rows(gdp_ctx* c, int b, const float* const* const* const* py) try {
+    if (!c || !py || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_upload_pyramid_rows: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    const Geom& g = c->geom;
+    std::vector<UpPiece> pieces;
+    for (int o = 0; o < g.O; ++o) {
+        const OctGeom& og = g.oct[o];
+        if ((size_t)og.rows * og.cols == 0) continue;
+        if (!py[o]) return c->status(GDP_ERR_ARG, "gdp_upload_pyramid_rows: null octave %d", o);
+        for (int s = 0; s < g.L; ++s) {
+            if (!py[o][s]) return c->status(GDP_ERR_ARG, "gdp_upload_pyramid_rows: null level (%d, %d)", o, s);
+            pieces.push_back({const_cast<float*>(gdp_device_level(c, b, o, s)), (size_t)og.cols, (size_t)og.rows, py[o][s]});
+        }
+    }
+    return stage_upload(c, pieces);
+} GDP_ABI_CATCH(c)
+
+int gdp_upload_image_raw(gdp_ctx* c, int b, const float* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_raw: bad argument") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, host, (size_t)c->geom.pyr_stride * 4,
+                              hipMemcpyHostToDevice, c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
 int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) try {
     if (!c || !host || o < 0 || o >= c->geom.O || s < 0 || s >= c->geom.L || (axis != 0 && axis != 1))
         return c ? c->status(GDP_ERR_ARG, "gdp_get_taps: bad argument") : GDP_ERR_ARG;
@@ -1501,6 +1660,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_CONV_WAVES: *value = c->conv_waves; return GDP_OK;
         case GDP_TUNE_ZERO_WINDOW: *value = c->zero_window; return GDP_OK;
         case GDP_TUNE_STORE_PACE: *value = c->geom.store_pace; return GDP_OK;
+        case GDP_TUNE_INPLACE_PACE: *value = c->geom.inplace_pace; return GDP_OK;
         case GDP_TUNE_CONV_PACE: *value = c->geom.conv_pace; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
@@ -1536,29 +1696,25 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             if (value < 0 || value > 2)
                 return c->status(GDP_ERR_ARG, "conv kernel must be 0 (sweep), 1 (LDS tiles) or 2 (block tiles)");
             c->conv_kernel = value;
-            return GDP_OK;
+            return conv_follow_rows(c);
         case GDP_TUNE_CONV_ROWS: {
             if (value != 8 && value != 16 && value != 24 && value != 32 && value != 48)
                 return c->status(GDP_ERR_ARG, "conv rows must be 8, 16, 24, 32 or 48 (sweep: 16 / 32; block tiles: "
                                               "16 / 32 / 48 with 16 waves, 8 / 16 / 24 / 32 with 8)");
-            const int old = c->conv_rows;
-            c->conv_rows = value;
-            conv_sweep_geom(c);
-            const int rc = upload_geom(c);
-            if (rc != GDP_OK) {
-                c->conv_rows = old;
-                conv_sweep_geom(c);
-            }
+            const int rc = conv_set_rows(c, value);
+            if (rc == GDP_OK) c->conv_rows_set = true;
             return rc;
         }
         case GDP_TUNE_CONV_WAVES:
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
             c->conv_waves = value;
-            return GDP_OK;
+            return conv_follow_rows(c);
         case GDP_TUNE_STORE_PACE:
-        case GDP_TUNE_CONV_PACE: {
+        case GDP_TUNE_CONV_PACE:
+        case GDP_TUNE_INPLACE_PACE: {
             if (value < -1 || value > 3) return c->status(GDP_ERR_ARG, "store pace must be -1 (off) or 0..3");
-            int& field = key == GDP_TUNE_STORE_PACE ? c->geom.store_pace : c->geom.conv_pace;
+            int& field = key == GDP_TUNE_STORE_PACE ? c->geom.store_pace
+                         : key == GDP_TUNE_CONV_PACE ? c->geom.conv_pace : c->geom.inplace_pace;
             const int old = field;
             field = value;
             const int rc = upload_geom(c);

@@ -243,7 +243,7 @@ class PyramidContext:
 
     _TUNING = ("nontemporal", "blocks_per_cu", "grid", "variant", "tile_order", "inplace_sub", "window_sub",
                "conv_kernel", "conv_rows", "conv_order", "build_lds", "stage_kb", "stage_threads", "conv_waves", "zero_window",
-               "store_pace", "conv_pace")
+               "store_pace", "conv_pace", "inplace_pace")
 
     @staticmethod
     def _tuning_key(name):
@@ -254,7 +254,7 @@ class PyramidContext:
     def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None,
                    inplace_sub=None, window_sub=None, conv_kernel=None, conv_rows=None, conv_order=None,
                    build_lds=None, stage_kb=None, stage_threads=None, conv_waves=None, zero_window=None,
-                   store_pace=None, conv_pace=None):
+                   store_pace=None, conv_pace=None, inplace_pace=None):
         """Performance knobs of the kernels (outputs are bit-identical for every setting; the
         conv_* knobs select the convolution extension's kernel: 0 register sweep, 1 LDS tiles,
         2 block tiles, and the sweep's rows per wave strip (16 / 32) or the block tiles' rows per
@@ -262,12 +262,13 @@ class PyramidContext:
         32 rows — any other pair makes build_gaussian raise GdpError); stage_kb / stage_threads
         size the double-buffered pinned staging of the row-pointer downloads; zero_window = 1 lets the
         build store the input-independent levels of pixels outside every window's support without
-        waiting for their input)."""
+        waiting for their input; store_pace / conv_pace / inplace_pace pace the stores of the
+        builds / the convolution block tiles / the in-place re-entry, each its own field)."""
         vals = dict(nontemporal=nontemporal, blocks_per_cu=blocks_per_cu, grid=grid, variant=variant,
                     tile_order=tile_order, inplace_sub=inplace_sub, window_sub=window_sub, conv_kernel=conv_kernel,
                     conv_rows=conv_rows, conv_order=conv_order, build_lds=build_lds, stage_kb=stage_kb,
                     stage_threads=stage_threads, conv_waves=conv_waves, zero_window=zero_window,
-                    store_pace=store_pace, conv_pace=conv_pace)
+                    store_pace=store_pace, conv_pace=conv_pace, inplace_pace=inplace_pace)
         for name in self._TUNING:
             if vals[name] is not None:
                 check(lib().gdp_set_tuning(self._ctx, self._tuning_key(name), int(vals[name])), self._ctx)
