@@ -8,6 +8,8 @@
 // (GaussDePyramid-HIP.h: constructor, GaussPy host mirror, GaussPyInit, output, destructor) and
 // differ only where the reference classes differ from GuassDePyramid.h:
 //
+// GaussPy is two-way state exactly as in GaussPyramid_hip (mirror_host / host_dirty / SyncDevice).
+//
 // GaussPyramid_a512omp_hip
 //  - GenerateDoG_nomp_dynamic() (:240-364), the path the reference times: scales 0..S-1 windowed
 //    with the integer-length centre float(len_o - 1) / 2 (:251, :279), then level i -= level i+1
@@ -53,6 +55,7 @@ public:
 };
 
 inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
+    pull_host_();  // GaussPy is two-way state (GaussDePyramid-HIP.h)
     check_(ctx_, fresh_ ? gdp_build_subset(ctx_, nullptr) : gdp_generate_dog_subset(ctx_, nullptr),
            "GenerateDoG_nomp_dynamic");
     fresh_ = false;
@@ -63,6 +66,7 @@ inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
 inline void GaussPyramid_a512omp_hip::GenerateDoG() {
     // per octave (:183-201): the DoG pass, then once more where the side is <= 2 — as two
     // launches, all octaves and then the tiny ones
+    pull_host_();
     int tiny = 0;
     while (tiny < layer && (length >> tiny) > 2) ++tiny;
     check_(ctx_, gdp_dog_range(ctx_, 0, layer, nullptr), "GenerateDoG");

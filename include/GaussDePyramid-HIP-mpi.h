@@ -26,12 +26,19 @@
 // :134-143 like GuassDePyramid.h (the two differ only when n is not a multiple of 2^(layer-1),
 // e.g. n = 100; pinned against the reference's own MPI runs, tests/golden/mpi_hashes.json).
 // Repeated calls continue from the current contents, like the reference's in-place methods:
-// right after GaussPyInit a call is the fused build of each band; after an earlier
-// GenerateDoG_mpi each band re-enters on its own rows (the op is pointwise, so this equals the
-// collector's whole-pyramid re-entry); after single-process calls (GaussFilter / GenerateDoG)
-// each rank applies GenerateDoG_mpi to its own GaussPy without communication — on the collector
-// that is the reference's result; workers, as in the reference, hold whatever their own calls
-// left.  Differences: MPI is initialised once (if the caller has not) and finalised by the
+// every call is collective (every rank builds its band and the collector gathers them).  A rank's
+// band starts from the fused build right after GaussPyInit, from its own rows of the last
+// GenerateDoG_mpi result (re-entry: the op is pointwise, so this equals the collector's whole-
+// pyramid re-entry), or — after single-process calls (GaussFilter / GenerateDoG) or host edits —
+// from its own rows of its whole-image state (gdp_copy_band).  GaussPy is two-way state, as in the
+// reference (GaussDePyramid-MPI.h:18, the float**** every method works on): with `mirror_host`
+// (default) a rank whose GaussPy mirrors its device state (every rank after GaussPyInit and the
+// single-process calls, the collector after GenerateDoG_mpi) uploads it before each mutating call,
+// so edits are processed; a worker's GaussPy is not refreshed by GenerateDoG_mpi (its result rows
+// live in its band context), so it uploads only when the caller sets `host_dirty`.  In the
+// reference the collector's output depends only on the workers' states (scale i from rank i); here
+// on every rank's own rows — the same whenever the ranks hold the same GaussPy (SPMD callers).
+// Differences: MPI is initialised once (if the caller has not) and finalised by the
 // destructor, so GenerateDoG_mpi may be called repeatedly (the reference calls
 // MPI_Init/MPI_Finalize inside and cannot); errors abort with a message instead of continuing.
 #ifndef SIFT_GAUSSDEPYRAMID_HIP_MPI_H
@@ -72,6 +79,10 @@ public:
     int chunk_size;
     int all_time;
     int rank() const { return rank_; }
+    bool mirror_host = true;  // two-way GaussPy (see the header comment)
+    bool host_dirty = false;  // the caller edited GaussPy / data: upload before the next call
+    void SyncHost() { sync_host_(); host_current_ = true; }
+    void SyncDevice();        // upload GaussPy into this rank's whole-image state now
 
 protected:
     int length;
@@ -86,6 +97,21 @@ protected:
     bool owns_mpi_;
     bool fresh_;      // contents == GaussPyInit() on every rank
     bool band_live_;  // band_ holds this rank's rows of the last GenerateDoG_mpi result
+    bool host_current_ = true;  // GaussPy mirrors full_ (false on workers after GenerateDoG_mpi)
+    bool rows_in_mirror_() const {
+        if (!host_) return false;
+        for (int o = 0; o < layer; ++o)
+            for (int s = 0; s < S + 3; ++s) {
+                const float* lev = host_ + gdp_level_offset(full_, 0, o, s);
+                const int n = length >> o;
+                for (int r = 0; r < n; ++r)
+                    if (GaussPy[o][s][r] != lev + (size_t)r * n) return false;
+            }
+        return true;
+    }
+    void pull_host_() {
+        if ((mirror_host && host_current_) || host_dirty) SyncDevice();
+    }
     // the error text is read only after the failing call returned (never as a sibling argument,
     // whose evaluation order relative to the call is unspecified)
     static void check_(int status, const char* what, const gdp_ctx* c) {
@@ -104,7 +130,7 @@ protected:
     }
     float* host_ = nullptr;  // pinned device-layout mirror the GaussPy rows point into (NULL: new[] rows)
     void sync_host_() {
-        check_(host_ ? gdp_download_image_raw(full_, 0, host_) : gdp_download_pyramid_rows(full_, 0, GaussPy),
+        check_(rows_in_mirror_() ? gdp_download_image_raw(full_, 0, host_) : gdp_download_pyramid_rows(full_, 0, GaussPy),
                "download", full_);
     }
     void ensure_full_();
@@ -165,25 +191,47 @@ inline void GaussPyramid_hip_mpi::ensure_full_() {  // the whole-image context o
     check_(gdp_set_input_rows(full_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit", full_);
 }
 
-inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GPU)
+inline void GaussPyramid_hip_mpi::SyncDevice() {
+    check_(rows_in_mirror_() ? gdp_upload_image_raw(full_, 0, host_)
+                             : gdp_upload_pyramid_rows(full_, 0, (const float* const* const* const*)GaussPy),
+           "SyncDevice", full_);
+    host_dirty = false;
+    host_current_ = true;
+    fresh_ = band_live_ = false;  // the caller's contents: bands start from this rank's rows of them
+}
+
+inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GPU), from the CURRENT `data`
+    const bool constructing = !is_initialized;  // the constructor just uploaded `data`
     ensure_full_();
+    if (!constructing && (mirror_host || host_dirty)) {
+        check_(gdp_set_input_rows(full_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit", full_);
+        int r0 = 0;  // the band's first input row
+        if (band_ && gdp_level_dims(band_, 0, nullptr, nullptr, &r0) == GDP_OK)
+            check_(gdp_set_input_rows(band_, 0, (const int32_t* const*)(data + r0), nullptr), "GaussPyInit", band_);
+    }
+    host_dirty = false;
     check_(gdp_init(full_, nullptr), "GaussPyInit", full_);
     is_initialized = true;
     fresh_ = true;
     band_live_ = false;
-    sync_host_();
+    if (mirror_host) SyncHost();
+    else host_current_ = false;
 }
 
 inline void GaussPyramid_hip_mpi::GaussFilter(int theLayer) {  // :133-167
+    pull_host_();
     check_(gdp_gauss_octave(full_, theLayer, nullptr), "GaussFilter", full_);
     fresh_ = band_live_ = false;
-    sync_host_();
+    if (mirror_host) SyncHost();
+    else host_current_ = false;
 }
 
 inline void GaussPyramid_hip_mpi::GenerateDoG() {  // :169-183 (single process, current contents)
+    pull_host_();
     check_(gdp_generate_dog(full_, nullptr), "GenerateDoG", full_);
     fresh_ = band_live_ = false;
-    sync_host_();
+    if (mirror_host) SyncHost();
+    else host_current_ = false;
 }
 
 inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :265-335
@@ -213,22 +261,23 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
                    band_);
         }
     }
-    if (!fresh_ && !band_live_) {
-        // single-process calls changed GaussPy since the last collective: every rank (all take
-        // this branch: the API is SPMD) applies GenerateDoG_mpi's filter + DoG to its own
-        // contents, the collector's being the reference's collector state
-        check_(gdp_set_window_centre(full_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi", full_);
-        check_(gdp_generate_dog(full_, nullptr), "GenerateDoG_mpi", full_);
-        check_(gdp_set_window_centre(full_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi", full_);
-        sync_host_();
-        return;
+    pull_host_();
+    // every rank takes the same (collective) path; only where its band starts from differs
+    if (band_) {
+        if (fresh_) {
+            check_(gdp_build(band_, nullptr), "GenerateDoG_mpi", band_);
+        } else {
+            if (!band_live_)  // single-process calls or host edits since: this rank's rows of full_
+                check_(gdp_copy_band(band_, 0, full_, 0, nullptr), "GenerateDoG_mpi", band_);
+            check_(gdp_generate_dog(band_, nullptr), "GenerateDoG_mpi", band_);
+        }
     }
-    if (band_) check_(fresh_ ? gdp_build(band_, nullptr) : gdp_generate_dog(band_, nullptr), "GenerateDoG_mpi", band_);
     check_comm_(gdp_comm_gather_bands(comm_, band_, 0, rank_ == 0 ? full_ : nullptr, 0, 0, nullptr), "GenerateDoG_mpi",
                 comm_);
     fresh_ = false;
     band_live_ = true;
-    if (rank_ == 0) sync_host_();
+    if (rank_ == 0 && mirror_host) SyncHost();
+    else host_current_ = false;  // workers: the result rows live in the band context
 }
 
 inline void GaussPyramid_hip_mpi::output() {  // :116-131

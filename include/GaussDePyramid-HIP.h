@@ -18,10 +18,20 @@
 //    it twice without GaussPyInit() filters twice, like the timing loop of main.cpp:66-73;
 //  - GaussPy holds [layer][S+3][len_o][len_o] floats allocated with new[] (:63-72), freed by the
 //    destructor (:151-170).
-// Differences: the reference never reports errors; a failing libgdp call here prints
-// gdp_last_error() and aborts rather than continuing on bad state.  After each mutating call
-// the device pyramid is copied back into GaussPy (PCIe traffic of the whole pyramid) unless
-// `mirror_host` is set to false, in which case call SyncHost() before reading GaussPy.
+// GaussPy is two-way state, as in the reference, where the float**** IS the pyramid and every
+// method works on whatever the caller left in it (:16, :122-131, :140-146):
+//  - mirror_host = true (default): before each mutating call (GaussFilter, GenerateDoG,
+//    GenerateDoG_mpi) the host GaussPy is uploaded to the device, and after it the device pyramid
+//    is copied back into GaussPy; GaussPyInit re-reads `data` (:80).  A caller may write
+//    g.GaussPy[o][s][r][c] (or g.data[r][c]) at any time and the next call processes the edit.
+//    Cost: one pyramid H2D + one D2H per call (PCIe; 447 MB each way at 4096^2).
+//  - mirror_host = false: the device pyramid is the state; GaussPy is refreshed only by
+//    SyncHost(), and host edits reach the device only through SyncDevice() — or set
+//    `host_dirty = true` after editing and the next mutating call uploads first (then clears it).
+// Row pointers the caller re-seated (GaussPy[o][s][r] = other array) are honoured both ways: the
+// single raw DMA copy is used only while every row still points into the pinned mirror.
+// Errors: the reference never reports them; a failing libgdp call here prints gdp_last_error()
+// and aborts rather than continuing on bad state.
 #ifndef SIFT_GAUSSDEPYRAMID_HIP_H
 #define SIFT_GAUSSDEPYRAMID_HIP_H
 
@@ -60,8 +70,10 @@ public:
     void GenerateDoG_mgpu(int argc, char** argv) { GenerateDoG_mpi(argc, argv); }  // SURVEY §8(f2) name
     ~GaussPyramid_hip();
     bool initialized;
-    bool mirror_host;  // copy the pyramid into GaussPy after every mutating call (default true)
+    bool mirror_host;  // GaussPy two-way: upload before / download after every mutating call (default true)
+    bool host_dirty;   // mirror_host == false: the caller edited GaussPy / data; the next call uploads first
     void SyncHost();   // copy the device pyramid into GaussPy now
+    void SyncDevice(); // copy GaussPy (the host pyramid, possibly edited) into the device pyramid now
     gdp_ctx* context() const { return ctx_; }
 
 protected:
@@ -73,6 +85,20 @@ protected:
     bool fresh_;  // contents == GaussPyInit(): GenerateDoG may use the fused build kernel
     float* host_; // pinned host pyramid in the device layout that the GaussPy rows point into
                   // (gdp_host_alloc); NULL: rows are separate new[] arrays (pinned memory refused)
+    bool rows_in_mirror_() const {  // every GaussPy row still where the constructor put it
+        if (!host_) return false;
+        for (int o = 0; o < layer; ++o)
+            for (int s = 0; s < S + 3; ++s) {
+                const float* lev = host_ + gdp_level_offset(ctx_, 0, o, s);
+                const int n = length >> o;
+                for (int r = 0; r < n; ++r)
+                    if (GaussPy[o][s][r] != lev + (size_t)r * n) return false;
+            }
+        return true;
+    }
+    void pull_host_() {  // before a mutating call: the caller's GaussPy is the state
+        if (mirror_host || host_dirty) SyncDevice();
+    }
     static void check_(gdp_ctx* c, int status, const char* what) {
         if (status != GDP_OK) {
             std::fprintf(stderr, "GaussPyramid_hip::%s failed: %s (%s)\n", what, gdp_status_string(status),
@@ -83,12 +109,12 @@ protected:
 };
 
 inline GaussPyramid_hip::GaussPyramid_hip()
-    : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), length(0), S(0), layer(0),
-      filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {}
+    : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), host_dirty(false), length(0), S(0),
+      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {}
 
 inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device)
-    : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), length(len), S(S_), layer(0),
-      filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {
+    : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), host_dirty(false), length(len), S(S_),
+      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {
     data = new int*[len];
     for (int i = 0; i < len; ++i) {
         data[i] = new int[len];
@@ -113,14 +139,29 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
             for (int r = 0; r < n; ++r) GaussPy[o][s][r] = lev ? lev + (size_t)r * n : new float[n];
         }
     }
-    GaussPyInit();
+    check_(ctx_, gdp_init(ctx_, nullptr), "GaussPyramid_hip");  // GaussPyInit (:57); `data` just uploaded
+    initialized = true;
+    fresh_ = true;
+    if (mirror_host) SyncHost();
 }
 
 inline void GaussPyramid_hip::SyncHost() {  // one DMA copy (pinned mirror) or one staged copy per 64 MiB
-    check_(ctx_, host_ ? gdp_download_image_raw(ctx_, 0, host_) : gdp_download_pyramid_rows(ctx_, 0, GaussPy), "SyncHost");
+    check_(ctx_, rows_in_mirror_() ? gdp_download_image_raw(ctx_, 0, host_) : gdp_download_pyramid_rows(ctx_, 0, GaussPy),
+           "SyncHost");
 }
 
-inline void GaussPyramid_hip::GaussPyInit() {
+inline void GaussPyramid_hip::SyncDevice() {  // the inverse: one H2D DMA copy, or staged row gathers
+    check_(ctx_, rows_in_mirror_() ? gdp_upload_image_raw(ctx_, 0, host_)
+                                   : gdp_upload_pyramid_rows(ctx_, 0, (const float* const* const* const*)GaussPy),
+           "SyncDevice");
+    host_dirty = false;
+    fresh_ = false;  // the contents are the caller's now, not necessarily GaussPyInit's
+}
+
+inline void GaussPyramid_hip::GaussPyInit() {  // :60-87, from the CURRENT `data` (:80)
+    if (mirror_host || host_dirty)
+        check_(ctx_, gdp_set_input_rows(ctx_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
+    host_dirty = false;  // every level is refilled: host edits of GaussPy are overwritten, as in :76-86
     check_(ctx_, gdp_init(ctx_, nullptr), "GaussPyInit");
     initialized = true;
     fresh_ = true;
@@ -128,6 +169,7 @@ inline void GaussPyramid_hip::GaussPyInit() {
 }
 
 inline void GaussPyramid_hip::GaussFilter(int theLayer) {
+    pull_host_();
     check_(ctx_, gdp_gauss_octave(ctx_, theLayer, nullptr), "GaussFilter");
     fresh_ = false;
     if (mirror_host) SyncHost();
@@ -136,6 +178,7 @@ inline void GaussPyramid_hip::GaussFilter(int theLayer) {
 inline void GaussPyramid_hip::GenerateDoG() {
     // on freshly initialised contents the fused single-pass build is bit-identical to
     // GaussFilter + DoG in place; otherwise run the in-place pass on what is there
+    pull_host_();
     check_(ctx_, fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr), "GenerateDoG");
     fresh_ = false;
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG");
@@ -145,6 +188,7 @@ inline void GaussPyramid_hip::GenerateDoG() {
 inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
     // switching centres selects the other device tap table (no drain, no re-upload after the
     // first call); both calls below are ordered on the context's stream
+    pull_host_();
     check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi");
     const int rc = fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr);
     check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi");

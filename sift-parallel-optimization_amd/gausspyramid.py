@@ -10,6 +10,13 @@
     g.output()                      # print scale 0 of every octave (:89-104)
     g.GaussPy[o][s][r][c]           # the pyramid (downloaded lazily from the device)
 
+GaussPy is two-way state, as the reference's float**** is (:16; GaussFilter / GenerateDoG work
+on whatever the caller left in it, :122-131, :140-146): a level the caller touched through
+GaussPy[o][s] is a host array that may be written (g.GaussPy[o][s][r][c] = v, row slices,
+whole-level assignment), and every mutating call first uploads each such level back to the device
+(gdp_upload_level), so the edit is processed; GaussPyInit re-reads the CURRENT `data` (:80).
+Levels never touched cost nothing.  SyncDevice() uploads them on demand.
+
 Calling GenerateDoG() twice without GaussPyInit() re-filters the pyramid exactly like the
 reference's timing loop does (main.cpp:66-73).  The one behavioural difference is error
 handling: the reference never reports errors (all methods return void); here a failing call
@@ -325,6 +332,15 @@ class PyramidContext:
         check(lib().gdp_download_pyramid(self._ctx, int(b), _ptr(out)), self._ctx)
         return out
 
+    def upload_level(self, b, o, s, arr):
+        """Copy a dense rows x cols float32 host array into level (o, s) of image b."""
+        rows, cols, _ = self._dims[o]
+        arr = np.ascontiguousarray(arr, dtype=np.float32)
+        if arr.shape != (rows, cols):
+            raise ValueError(f"level ({o}, {s}) is {rows} x {cols}, got {arr.shape}")
+        if arr.size:
+            check(lib().gdp_upload_level(self._ctx, int(b), int(o), int(s), _ptr(arr)), self._ctx)
+
     def upload_pyramid(self, packed, b=0):
         packed = np.ascontiguousarray(packed, dtype=np.float32)
         if packed.size != self.packed_floats():
@@ -392,6 +408,9 @@ class _LevelView:
     def __getitem__(self, s):
         return self._owner._level(self._o, s)
 
+    def __setitem__(self, s, value):  # GaussPy[o][s] = array: the level's new contents
+        self._owner._level(self._o, s)[...] = value
+
     def __len__(self):
         return self._owner.S + 3
 
@@ -412,14 +431,14 @@ class GaussPyramid:
         self.S = int(S)
         self.layer = octaves_for(length)  # :48-53
         self._ctx = PyramidContext(length, length, self.S, self.layer, batch=1, device=device)
-        self._ctx.set_input(self.data)
         self._cache = {}
         self._fresh = False
         self.GaussPyInit()  # :57
 
     # reference surface -------------------------------------------------------
     def GaussPyInit(self):
-        """:60-87 — refill every level of every octave with the decimated input."""
+        """:60-87 — refill every level of every octave with the decimated CURRENT `data` (:80)."""
+        self._ctx.set_input(self.data)
         self._ctx.init()
         self.initialized = True
         self._fresh = True  # contents == init, so GenerateDoG may take the fused path
@@ -427,12 +446,14 @@ class GaussPyramid:
 
     def GaussFilter(self, theLayer):
         """:106-134 — multiply every scale of octave `theLayer` by its window, in place."""
+        self.SyncDevice()
         self._ctx.gauss_octave(int(theLayer))
         self._fresh = False
         self._cache.clear()
 
     def GenerateDoG(self):
         """:136-149 — GaussFilter + DoG for every octave, in place on the current contents."""
+        self.SyncDevice()
         if self._fresh:
             self._ctx.build()  # fused init+filter+DoG: bit-identical to the in-place sequence
         else:
@@ -454,6 +475,16 @@ class GaussPyramid:
     @property
     def GaussPy(self):
         return [_LevelView(self, o) for o in range(self.layer)]
+
+    def SyncDevice(self):
+        """Upload every level the caller obtained through GaussPy (and so may have written) into the
+        device pyramid; the next call processes the host contents."""
+        if not self._cache:
+            return
+        for (o, s), arr in self._cache.items():
+            self._ctx.upload_level(0, o, s, arr)
+        self._cache.clear()
+        self._fresh = False  # the caller's contents, not necessarily GaussPyInit's
 
     # helpers -----------------------------------------------------------------
     def _level(self, o, s):
@@ -490,6 +521,7 @@ class GaussPyramid_a512omp(GaussPyramid):
     def GenerateDoG(self):
         """:183-213 — DoG pass only (level j -= level j+1, j = 0..S+1) per octave, twice on octaves
         of side <= 2."""
+        self.SyncDevice()
         self._ctx.dog_range(0, self.layer)  # one launch for every octave ...
         tiny = next((o for o in range(self.layer) if self.length >> o <= 2), self.layer)
         if tiny < self.layer:
@@ -499,6 +531,7 @@ class GaussPyramid_a512omp(GaussPyramid):
 
     def GenerateDoG_nomp_dynamic(self):
         """:240-364 — scales 0..S-1 windowed, DoG for i < S-1: {DoG_0..DoG_{S-2}, G_{S-1}, x, x, x}."""
+        self.SyncDevice()
         if self._fresh:
             self._ctx.build_subset()
         else:

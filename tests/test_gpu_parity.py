@@ -498,6 +498,32 @@ def test_conv_block_tiles_refuse_uninstantiated_pairs(pkg):
         ctx.sync()
 
 
+def test_conv_single_knob_selections_run(pkg):
+    """rows the caller never set follow the selected kernel / waves (the sweep's 16-row
+    strips, 32 rows on 8 waves, 48 on 16), so setting ONLY conv_kernel = 0 or ONLY conv_waves = 8
+    builds — and agrees with the default block tiles within the extension's tolerance (one
+    convolution, other tilings: |a - b| <= 1e-3 + 1e-5 |b|)."""
+    def run(**knobs):
+        with pkg.PyramidContext(256, 256, S=2, octaves=3) as ctx:
+            ctx.fill_synthetic(7, 0)
+            ctx.set_tuning(**knobs)
+            ctx.build_gaussian()
+            ctx.sync()
+            return ctx.tuning()["conv_rows"], ctx.pyramid(0)
+
+    rows0, ref = run()
+    assert rows0 == 48
+    for knobs, rows in (({"conv_kernel": 0}, 16), ({"conv_waves": 8}, 32), ({"conv_kernel": 0, "conv_waves": 8}, 16),
+                        ({"conv_waves": 8, "conv_kernel": 2}, 32)):
+        got_rows, got = run(**knobs)
+        assert got_rows == rows, knobs
+        assert np.all(np.abs(got.astype(np.float64) - ref) <= 1e-3 + 1e-5 * np.abs(ref.astype(np.float64))), knobs
+    with pkg.PyramidContext(256, 256, S=2, octaves=3) as ctx:  # an explicit row count is kept
+        ctx.set_tuning(conv_rows=32)
+        ctx.set_tuning(conv_kernel=0)
+        assert ctx.tuning()["conv_rows"] == 32
+
+
 # ------------------------------------------------------------------ full-size properties
 def test_config3_batch_1080p(pkg, oracle):
     """64 x 1080x1920, 5 octaves (BASELINE config 3) — a spread of images checked exactly."""

@@ -1,0 +1,229 @@
+"""GaussPy as two-way state.
+
+In the reference, `float**** GaussPy` IS the pyramid: GaussFilter / GenerateDoG work on whatever
+the caller left in it (GuassDePyramid.h:16, :122-131, :140-146), and GaussPyInit re-reads `data`
+(:80).  These tests edit the drop-ins' GaussPy (C++ classes through examples/state_hip, the Python
+mirror directly) between calls — a level zeroed, a row scaled, a level negated, single values up
+to FLT_MAX, a re-seated row pointer, an edited input pixel — and require the result to be
+bit-identical (0 ULP) to the oracle's in-place restatement (gauss_octave / generate_dog /
+GenerateDoG_nomp_dynamic's subset) applied to the same edited pyramid.  Runs on an MI355X.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "examples", "state_hip")
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _assert_same(got, want, what):
+    g, w = _bits(got), _bits(want)
+    assert g.shape == w.shape, (what, g.shape, w.shape)
+    bad = np.flatnonzero(g.ravel() != w.ravel())
+    assert bad.size == 0, f"{what}: {bad.size} words differ, first at {bad[:5]}"
+
+
+class _Replay:
+    """The oracle side of a state_hip op list: the same edits and calls on a packed pyramid."""
+
+    def __init__(self, oracle, cls, n, S, spec):
+        self.o, self.cls, self.n, self.S = oracle, cls, n, S
+        self.O = oracle.octaves(n)
+        self.img = oracle.image_from_spec(n, spec).astype(np.int32)
+        self.pyr = oracle.init_pyramid(self.img, S)
+        self.mirror, self.dirty = True, False
+        self.host = self.pyr.copy()  # what GaussPy holds on the host
+
+    def _lv(self, pyr, o, s):
+        return self.o.levels(pyr, self.n, self.n, self.S, self.O)[(o, s)]
+
+    def _pull(self):  # before a mutating call: GaussPy is uploaded when mirrored or flagged
+        if self.mirror or self.dirty:
+            self.pyr[:] = self.host
+            self.dirty = False
+
+    def _push(self):
+        if self.mirror:
+            self.host[:] = self.pyr
+
+    def apply(self, op):
+        f = op.split(":")
+        n, S, O, o = self.n, self.S, self.O, self.o
+        intlen = "intlen" if self.cls in ("a512omp", "a512xp") else "serial"
+        if f[0] == "init":
+            self.pyr[:] = o.init_pyramid(self.img, S)
+            self.dirty = False
+            self._push()
+        elif f[0] in ("dog", "mpi", "nomp", "filter"):
+            self._pull()
+            if f[0] == "filter":
+                if self.cls != "a512omp":  # that class's GaussFilter is empty (:128-181)
+                    o.gauss_octave(self.pyr, n, n, S, int(f[1]))
+            elif f[0] == "mpi":
+                o.generate_dog(self.pyr, n, n, S, O, centre="intlen")
+            elif f[0] == "nomp":
+                o.subset_a512omp(self.pyr, n, n, S, O)
+            elif self.cls == "a512omp":
+                o.generate_dog_a512omp(self.pyr, n, n, S, O)
+            else:
+                o.generate_dog(self.pyr, n, n, S, O, centre=intlen)
+            self._push()
+        elif f[0] == "mirror":
+            self.mirror = f[1] == "1"
+        elif f[0] == "dirty":
+            self.dirty = True
+        elif f[0] == "syncdev":
+            self.pyr[:] = self.host
+            self.dirty = False
+        elif f[0] == "synchost":
+            self.host[:] = self.pyr
+        elif f[0] == "data":
+            self.img[int(f[1]), int(f[2])] = int(f[3])
+        elif f[0] == "reseat":
+            pass  # same contents, another address
+        else:
+            lv = self._lv(self.host, int(f[1]), int(f[2]))
+            if f[0] == "zero":
+                lv[:] = 0.0
+            elif f[0] == "neg":
+                lv[:] = -lv
+            elif f[0] == "scale":
+                lv[int(f[3])] *= np.float32(float(f[4]))
+            elif f[0] == "set":
+                lv[int(f[3]), int(f[4])] = np.float32(float(f[5]))
+        return self
+
+
+def _assert_same_nan(got, want, what):
+    """Bit-exact except NaN payloads: inf * 0 gives the default NaN of the machine that computes
+    it (x86 SSE: 0xFFC00000, gfx950: 0x7FC00000), so NaNs compare by position only."""
+    g, w = _bits(got).copy(), _bits(want).copy()
+    gn, wn = np.isnan(g.view(np.float32)), np.isnan(w.view(np.float32))
+    assert np.array_equal(gn, wn), (what, "NaN positions differ", np.flatnonzero(gn != wn)[:5])
+    g[gn] = w[wn] = 0x7FC00000
+    _assert_same(g.view(np.float32), w.view(np.float32), what)
+
+
+def _run(oracle, tmp_path, cls, n, S, spec, ops):
+    if not os.path.exists(EXE):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
+    out = tmp_path / "state.f32"
+    subprocess.run([EXE, cls, str(n), str(S), spec, str(out), *ops], check=True, timeout=120)
+    rp = _Replay(oracle, cls, n, S, spec)
+    for op in ops:
+        rp.apply(op)
+    _assert_same(np.fromfile(out, dtype=np.float32), rp.host, (cls, n, S, ops))
+
+
+EDITS = ["zero:0:1", "scale:0:2:5:-3.5", "neg:1:0", "set:0:0:3:7:-1e30", "set:2:3:1:1:3.0e38"]
+
+
+@pytest.mark.parametrize("n,S", [(64, 2), (100, 2), (96, 3)])
+def test_cpp_class_processes_host_edits(oracle, tmp_path, n, S):
+    """GaussPyramid_hip with the default mirror_host: edits of GaussPy between calls are what
+    GaussFilter / GenerateDoG / GenerateDoG_mpi process, and GaussPyInit discards them."""
+    _run(oracle, tmp_path, "hip", n, S, "lcg:3", EDITS + ["filter:0", "filter:1", "neg:0:4", "dog"])
+    _run(oracle, tmp_path, "hip", n, S, "lcg:4", ["dog"] + EDITS + ["dog", "scale:1:1:0:0.25", "mpi"])
+    _run(oracle, tmp_path, "hip", n, S, "lcg:5", EDITS + ["init", "dog"])  # refill overwrites the edits
+    _run(oracle, tmp_path, "hip", n, S, "lcg:6", ["data:3:5:-70000", "data:0:0:2147483647", "init", "zero:0:4", "dog"])
+
+
+def test_cpp_class_without_mirror_uploads_only_when_told(oracle, tmp_path):
+    """mirror_host = false: the device pyramid is the state; host edits reach it only through
+    host_dirty (next call uploads first) or SyncDevice(), and SyncHost() overwrites the host."""
+    n, S = 64, 2
+    _run(oracle, tmp_path, "hip", n, S, "lcg:7", ["mirror:0", "zero:0:1", "dog", "synchost"])  # edit never uploaded
+    _run(oracle, tmp_path, "hip", n, S, "lcg:7", ["mirror:0", "zero:0:1", "dirty", "dog", "synchost"])
+    _run(oracle, tmp_path, "hip", n, S, "lcg:7", ["mirror:0", "neg:0:2", "syncdev", "filter:0", "synchost"])
+    _run(oracle, tmp_path, "hip", n, S, "lcg:7", ["mirror:0", "dog", "synchost", "scale:0:0:31:2", "dirty", "dog",
+                                                  "synchost"])
+
+
+def test_cpp_class_honours_reseated_rows(oracle, tmp_path):
+    """A caller may point GaussPy[o][s][r] at another array (the reference's rows are separate
+    new[] arrays): both directions then go through the staged row copies, not the raw mirror."""
+    _run(oracle, tmp_path, "hip", 64, 2, "lcg:8", ["reseat:0:1:7", "scale:0:1:7:-2", "dog", "scale:0:0:7:4", "dog"])
+    _run(oracle, tmp_path, "hip", 100, 2, "lcg:9", ["reseat:2:0:0", "reseat:0:4:99", "set:0:4:99:50:1e20", "filter:0",
+                                                    "filter:2", "dog"])
+
+
+def test_cpp_avx512_classes_process_host_edits(oracle, tmp_path):
+    """GaussPyramid_a512omp_hip (GenerateDoG_nomp_dynamic's subset; GenerateDoG = DoG only) and
+    GaussPyramid_a512xp_hip (integer-length GenerateDoG, serial GaussFilter) on edited state."""
+    for n in (64, 8):
+        _run(oracle, tmp_path, "a512omp", n, 2, "lcg:10", ["zero:0:0", "neg:0:3", "nomp", "scale:0:1:2:3", "nomp"])
+        _run(oracle, tmp_path, "a512omp", n, 2, "lcg:11", ["neg:0:2", "dog", "filter:0", "set:1:4:1:1:-5", "dog"])
+        _run(oracle, tmp_path, "a512xp", n, 2, "lcg:12", ["zero:1:1", "scale:0:0:1:-1", "dog", "neg:0:0", "filter:0",
+                                                          "dog"])
+
+
+def test_python_mirror_processes_host_edits(pkg, oracle):
+    """The Python GaussPyramid: writes through GaussPy[o][s] (element, row, whole level) and into
+    `data` are processed by the next call, like the reference's float**** and data copy."""
+    n, S = 100, 2
+    O = oracle.octaves(n)
+    img = oracle.lcg_image(n, n, 21)
+    g = pkg.GaussPyramid(img, n, S)
+    want = oracle.init_pyramid(img, S)
+    lv = lambda p, o, s: oracle.levels(p, n, n, S, O)[(o, s)]  # noqa: E731
+    g.GaussPy[0][1][5] *= np.float32(-3)
+    lv(want, 0, 1)[5] *= np.float32(-3)
+    g.GaussPy[1][0] = np.full((n >> 1, n >> 1), 2.5, np.float32)
+    lv(want, 1, 0)[:] = 2.5
+    g.GaussPy[0][3][10, 20] = np.float32(3e38)
+    lv(want, 0, 3)[10, 20] = np.float32(3e38)
+    g.GaussFilter(0)
+    oracle.gauss_octave(want, n, n, S, 0)
+    _assert_same(g.pyramid(), want, "python GaussFilter after edits")
+    g.GaussPy[0][0][:] = 0
+    lv(want, 0, 0)[:] = 0
+    g.GenerateDoG()
+    oracle.generate_dog(want, n, n, S, O)
+    _assert_same(g.pyramid(), want, "python GenerateDoG after edits")
+    g.data[7, 9] = -123456
+    img2 = img.copy()
+    img2[7, 9] = -123456
+    g.GaussPyInit()
+    g.GenerateDoG()
+    _assert_same(g.pyramid(), oracle.build_pyramid(img2, S), "python GaussPyInit re-reads data")
+    g.close()
+
+
+def test_inplace_zero_window_is_exact_for_caller_values_near_flt_max(pkg, oracle):
+    """with S >= 3 some column taps exceed 1, so for a row outside the window support
+    (fr = +0) v * fc can overflow to inf and inf * 0 = NaN — the zero-window shortcut of the
+    in-place passes must not turn that into a zero.  A caller-written 3e38 at such a pixel, then
+    GaussFilter / GenerateDoG re-entry with the knob on == the oracle (bits incl. NaN)."""
+    n, S = 255, 3  # odd side: the window centre falls on a pixel, where scale 5's tap is 1.197
+    O = oracle.octaves(n)
+    img = oracle.lcg_image(n, n, 5)
+    base = oracle.build_pyramid(img, S)
+    lv = lambda p, o, s: oracle.levels(p, n, n, S, O)[(o, s)]  # noqa: E731
+    c = (n - 1) // 2
+    assert oracle.taps(n, 0, S + 2)[c] > 1.0
+    for s in range(S + 3):
+        lv(base, 0, s)[0, c] = np.float32(3.0e38)   # row 0: outside every row window; column: centre
+        lv(base, 0, s)[1, c + 1] = np.float32(-3.0e38)
+        lv(base, 0, s)[c, 0] = np.float32(3.0e38)   # column 0 outside: exact either way
+    with pkg.PyramidContext(n, n, S=S) as ctx:
+        for zw in (0, 1):
+            ctx.set_tuning(zero_window=zw)
+            for sub, wsub in ((1, 4), (0, 1), (16, 16)):
+                ctx.set_tuning(inplace_sub=sub, window_sub=wsub)
+                ctx.upload_pyramid(base)
+                ctx.gauss_octave(0)
+                ctx.sync()
+                _assert_same_nan(ctx.pyramid(0), oracle.gauss_octave(base.copy(), n, n, S, 0), ("gauss", zw, sub, wsub))
+                ctx.upload_pyramid(base)
+                ctx.generate_dog()
+                ctx.sync()
+                _assert_same_nan(ctx.pyramid(0), oracle.generate_dog(base.copy(), n, n, S, O), ("regen", zw, sub))
+    assert np.isnan(lv(oracle.gauss_octave(base.copy(), n, n, S, 0), 0, S + 2)[0, c])  # the case exists
