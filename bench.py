@@ -171,6 +171,42 @@ def _ref_stamp(binary):
             "compiler": st.get("compiler"), "flags": st.get("flags"), "built_utc": st.get("built_utc")}
 
 
+def complete_line(result, args, rank, world, dist, mg, device, bytes_launch, wall):
+    """The parts of the line every N needs: the whole-job roofline — every
+    rank's algorithmic bytes per step over the job's step time, against N GPUs' peak
+    (`frac_aggregate`; `frac` is the per-launch rate of rank 0's kernel, its bytes over its launch)
+    — and the CPU baseline (attach_cpu_baseline).  Collective: every rank calls it."""
+    total = mg.sum_over_ranks(bytes_launch, dist=dist, device=device)
+    if rank == 0:
+        result["roofline"]["aggregate_bytes_per_step"] = total
+        result["roofline"]["frac_aggregate"] = round(total / (wall / args.steps) / (world * HBM_PEAK_GBS * 1e9), 4)
+    attach_cpu_baseline(result, args, rank, world, dist)
+
+
+def attach_cpu_baseline(result, args, rank, world, dist):
+    """The reference's CPU path timed on this box's host cores in the same run (north star), on
+    rank 0 only and after every rank's timed region: at N > 1 the other ranks wait at a barrier
+    until rank 0 has sampled it, so no GPU step overlaps the CPU sample and the line is complete at
+    every N (mpitest.cpp:95-96 times its collector in the same run)."""
+    if args.no_cpu:
+        if rank == 0:
+            result["cpu_baseline"] = None
+    elif rank == 0:
+        base = cpu_baseline(args.cpu_budget)
+        base["semantics_vs_this_line"] = {
+            "build": "the GPU line computes the full GenerateDoG output; the timed CPU path its subset (see sample); "
+                     "serial_full_semantics / a512xp_full_semantics are the full-output CPU rates",
+            "subset": "identical: the GPU line computes GenerateDoG_nomp_dynamic's output",
+            "conv": "none: the reference has no convolution (the extension has no CPU counterpart)",
+        }.get(args.op, "in-place pass vs the CPU build path (different work)")
+        if world > 1:
+            base["when"] = (f"rank 0, after all {world} ranks finished their timed steps; ranks 1..{world - 1} "
+                            f"waited at a barrier meanwhile (no GPU work during the sample)")
+        result["cpu_baseline"] = base
+    if dist is not None and world > 1:
+        dist.barrier()
+
+
 def latest_conv_pmc(config_key, tun):
     """PMC record of the convolution extension's kernel on this workload with the run's conv
     kernel / rows / order (profiles/pmc_<cfg>_conv*_*.json), or None."""
@@ -190,11 +226,13 @@ def latest_conv_pmc(config_key, tun):
     return best
 
 
-def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0):
+def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0, band_of=None):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
     whose recorded build variant, tile order and zero-window mode equal the run's; None when no profile of that
-    instance exists (the traffic of another variant would describe a different kernel)."""
+    instance exists (the traffic of another variant would describe a different kernel).  band_of = N:
+    the row-band config's per-rank launch at N ranks (rank 0's band of N, profiled on one GPU by
+    tools/pmc_variants.py --band-of N), not the whole image's."""
     pdir = os.path.join(REPO, "profiles")
     best = None
     if os.path.isdir(pdir):
@@ -210,7 +248,7 @@ def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_windo
                 if rec.get("config") == config_key and rec.get("op", "build") == op and \
                         rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
                         rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32" and \
-                        rec.get("zero_window", 0) == zero_window and \
+                        rec.get("zero_window", 0) == zero_window and rec.get("band_of") == band_of and \
                         lt in rec.get("kernel", lt):
                     best = dict(rec, file=f)
     return best
@@ -981,10 +1019,12 @@ def main():
         bytes_launch = algorithmic_bytes(H, W, S, O, B, in_bytes)
     achieved = bytes_launch / (kernel_ms / 1e3) / 1e9
     tun = ctx.tuning()
-    # PMC records are of the whole workload on one GPU: a row band (config 5 at N > 1) is another launch
+    # PMC records are of the whole workload on one GPU; a row band (config 5 at N > 1) is another
+    # launch, profiled separately as rank 0's band of N on one GPU (tools/pmc_variants.py --band-of N)
+    band_of = world if (cfg["band"] and world > 1) else None
     pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3,
-                      tun["zero_window"] if args.op == "build" else 0)
-           if args.op in ("build", "subset") and args.input == "i32" and not (cfg["band"] and world > 1) else None)
+                      tun["zero_window"] if args.op == "build" else 0, band_of=band_of)
+           if args.op in ("build", "subset") and args.input == "i32" and (band_of is None or rank == 0) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
     if args.op in ("regen", "gauss") and not (cfg["band"] and world > 1):
@@ -1073,16 +1113,7 @@ def main():
                                      " [op=subset: GaussPyramid_a512omp::GenerateDoG_nomp_dynamic's output, the "
                                      "CPU baseline's own semantics]" if args.op == "subset" else
                                      f" [op={args.op}: in-place pass]")
-    if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
-        result["cpu_baseline"]["semantics_vs_this_line"] = {
-            "build": "the GPU line computes the full GenerateDoG output; the timed CPU path its subset (see sample); "
-                     "serial_full_semantics / a512xp_full_semantics are the full-output CPU rates",
-            "subset": "identical: the GPU line computes GenerateDoG_nomp_dynamic's output",
-            "conv": "none: the reference has no convolution (the extension has no CPU counterpart)",
-        }.get(args.op, "in-place pass vs the CPU build path (different work)")
-    elif rank == 0:
-        result["cpu_baseline"] = None
+    complete_line(result, args, rank, world, dist, mg, red_dev, bytes_launch, wall)
     for c in ctxs:
         c.close()
     if rank == 0:

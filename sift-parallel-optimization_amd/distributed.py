@@ -139,6 +139,16 @@ def max_over_ranks(values, dist=None, device="cpu"):
     return [float(v) for v in t.cpu()]
 
 
+def sum_over_ranks(value, dist=None, device="cpu"):
+    """Sum of one integer over all ranks (exact in int64: the job's algorithmic bytes per step)."""
+    import torch
+
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.cpu()[0])
+
+
 def gather_checksums(local, dist=None, dst=0):
     """Gather each rank's list of 64-bit checksums to rank `dst` (None elsewhere)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:

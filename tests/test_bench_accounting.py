@@ -281,3 +281,47 @@ def test_cpu_baseline_provenance_stamp(tmp_path):
     assert st["sources_sha256"]["GuassDePyramid.h"] == hashlib.sha256(src.read_bytes()).hexdigest()
     binary.write_bytes(b"\x7fELF rebuilt without a new stamp")
     assert bench._ref_stamp(str(binary))["binary_matches_stamp"] is False
+
+
+_LINE_PROBE = r"""
+import json, os, sys, types
+sys.path.insert(0, sys.argv[1])
+import torch.distributed as dist
+import bench
+import __graft_entry__ as entry
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+dist.init_process_group("gloo", init_method="file://" + os.environ["GDP_BENCH_RDV"], rank=rank, world_size=world)
+mg = __import__(entry.load_package().__name__ + ".distributed", fromlist=["sum_over_ranks"])
+args = types.SimpleNamespace(steps=10, no_cpu=False, cpu_budget=0.2, op="build")
+result = {"roofline": {"frac": 0.75}}
+bytes_launch = 514_064_384 * (rank + 1)  # ranks may carry different shares (row bands)
+bench.complete_line(result, args, rank, world, dist, mg, "cpu", bytes_launch, 10 * 0.1e-3)
+if rank == 0:
+    with open(sys.argv[2], "w") as f:
+        json.dump(result, f)
+dist.destroy_process_group()
+"""
+
+
+def test_multi_rank_line_carries_cpu_baseline_and_aggregate_roofline(tmp_path):
+    """at N > 1 the line still carries `cpu_baseline` (rank 0 samples it after
+    every rank's timed region while the others wait at a barrier) and the whole-job
+    `frac_aggregate` = sum of every rank's algorithmic bytes / ms_per_step / (N x 8 TB/s) —
+    two self-launched gloo ranks (bench.launch_ranks, the driver's --gpus N path) through the
+    same bench.complete_line the GPU run calls."""
+    import json
+
+    import bench
+
+    probe = tmp_path / "probe.py"
+    probe.write_text(_LINE_PROBE)
+    out = tmp_path / "line.json"
+    assert bench.launch_ranks(2, [REPO, str(out)], script=str(probe)) == 0
+    line = json.loads(out.read_text())
+    total = 514_064_384 * 3
+    assert line["roofline"]["aggregate_bytes_per_step"] == total
+    assert line["roofline"]["frac_aggregate"] == round(total / 0.1e-3 / (2 * 8000e9), 4)
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["unit"] == "Mpix/s" and cb["cores"] >= 1 and cb["kind"] in ("reference", "port")
+    assert "after all 2 ranks finished their timed steps" in cb["when"]

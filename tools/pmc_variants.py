@@ -32,9 +32,11 @@ def run(args):
     pkg = entry.load_package()
     cfg = bench.CONFIGS[args.config]
     H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
-    set_bytes = bench.algorithmic_bytes(H, W, 2, O, B)
+    r0, r1 = band_rows(pkg, cfg, args.band_of)
+    set_bytes = band_bytes(cfg, r0, r1)
     rotate = max(1, -(-bench.ROTATE_BYTES // set_bytes))
-    ctxs = [pkg.PyramidContext(H, W, S=2, octaves=O, batch=B) for _ in range(rotate)]
+    # --band-of N: rank 0's row band of the N-rank row-band job (bench.py's context on that rank)
+    ctxs = [pkg.PyramidContext(H, W, S=2, octaves=O, batch=B, row_begin=r0, row_end=r1) for _ in range(rotate)]
     for c in ctxs:
         c.fill_synthetic(bench.SEED, 0)
         c.set_tuning(zero_window=args.zero_window)
@@ -63,7 +65,27 @@ def run(args):
         c.close()
     with open(args.manifest, "w") as f:
         json.dump({"config": args.config, "op": args.op, "rotate": rotate, "zero_window": args.zero_window,
-                   "instances": manifest}, f)
+                   "band_of": args.band_of, "band": [r0, r1], "instances": manifest}, f)
+
+
+def band_rows(pkg, cfg, band_of):
+    """Rows of the profiled context: the whole image, or rank 0's band of `band_of` ranks."""
+    if not band_of:
+        return 0, cfg["H"]
+    if not cfg["band"]:
+        sys.exit("--band-of needs the row-band config (c5)")
+    mg = __import__(pkg.__name__ + ".distributed", fromlist=["plan_band"])
+    return mg.plan_band(cfg["H"], band_of, 0, cfg["O"])
+
+
+def band_bytes(cfg, r0, r1):
+    """Algorithmic bytes of one launch over input rows [r0, r1): 4 B per input pixel + 4 (S+3) B
+    per pyramid pixel of the band (bench.py's per-rank accounting)."""
+    H, W, O, B = cfg["H"], cfg["W"], cfg["O"], cfg["batch"]
+    if (r0, r1) == (0, H):
+        return bench.algorithmic_bytes(H, W, 2, O, B)
+    px = sum((((r1 + (1 << o) - 1) >> o) - ((r0 + (1 << o) - 1) >> o)) * (W >> o) for o in range(O))
+    return B * (4 * (r1 - r0) * W + 4 * 5 * px)
 
 
 def per_dispatch(d, counter):
@@ -85,7 +107,9 @@ def summarise(args):
     if len(fetch) != total or len(write) != total:
         sys.exit(f"dispatch count mismatch: manifest {total}, FETCH_SIZE {len(fetch)}, WRITE_SIZE {len(write)}")
     cfg = bench.CONFIGS[man["config"]]
-    alg = bench.algorithmic_bytes(cfg["H"], cfg["W"], 2, cfg["O"], cfg["batch"])
+    band_of = man.get("band_of")
+    r0, r1 = man.get("band", [0, cfg["H"]])
+    alg = band_bytes(cfg, r0, r1)
     k = 0
     for m in man["instances"]:
         fs, ws = fetch[k:k + m["dispatches"]], write[k:k + m["dispatches"]]
@@ -96,6 +120,7 @@ def summarise(args):
         rec = {"config": man["config"], "round": args.round, "kernel": fs[0][2], "variant": m["variant"],
                "tile_order": m["tile_order"], "input_format": "i32", "op": man.get("op", "build"),
                "zero_window": man.get("zero_window", 0),
+               **({"band_of": band_of, "band_rows": [r0, r1]} if band_of else {}),
                "source": "tools/pmc_variants.py: every instance in one process, its own FETCH_SIZE and WRITE_SIZE "
                          "rocprofv3 --pmc passes, launches cycling over %d cold buffer sets as in bench.py" % man["rotate"],
                "dispatches_counted": [len(fs), len(ws)],
@@ -104,7 +129,7 @@ def summarise(args):
                "kernel_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
                "traffic_over_algorithmic": (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads); write = WRITE_SIZE KiB"}
-        tag = man["config"] + ("_subset" if man.get("op") == "subset" else "")
+        tag = man["config"] + (f"b{band_of}" if band_of else "") + ("_subset" if man.get("op") == "subset" else "")
         zw = "z1" if man.get("zero_window", 0) else ""
         out = os.path.join(REPO, "profiles", f"pmc_{tag}_v{m['variant']}o{m['tile_order']}{zw}_{args.round}.json")
         if os.path.exists(out) and not args.overwrite:
@@ -126,6 +151,9 @@ def main():
                     help="subset: the GenerateDoG_nomp_dynamic build (bench.py --op subset)")
     ap.add_argument("--zero-window", type=int, default=0, choices=[0, 1],
                     help="GDP_TUNE_ZERO_WINDOW of every instance (records pmc_<cfg>_v<V>o<T>z1_*.json)")
+    ap.add_argument("--band-of", type=int, default=None,
+                    help="row-band config: profile rank 0's band of N ranks (bench.py --gpus N --config c5's "
+                         "per-rank launch; records pmc_c5b<N>_*.json)")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--round", default="r02")
