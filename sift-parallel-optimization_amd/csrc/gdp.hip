@@ -161,6 +161,33 @@ namespace {
 // Tile grid of the selected build variant (tile width differs per variant).
 int retile(gdp_ctx* c, int tile_cols, int tile_rows) {
     Geom& g = c->geom;
+    if (tile_rows == 0) {
+        // Contiguous-span variants (PATH 4): every octave's groups, in row-major
+        // order (the levels are dense row-major, GuassDePyramid.h:63-72), are cut into the same
+        // number of contiguous chunks, one per work unit — octave 0 into chunks of at most
+        // `tile_cols` groups, octave o into proportional ones, which read the same input rows.
+        // A unit's stores are then one contiguous span of each level, crossing row boundaries,
+        // instead of tile rows a row pitch apart.  No tail units: every octave lives in the units.
+        const long long total0 = (long long)g.oct[0].rows * g.oct[0].gpr;
+        const long long nblk = std::max(1ll, (total0 + tile_cols - 1) / tile_cols);
+        long long rest = 0;
+        for (int o = 0; o < g.O; ++o) {
+            OctGeom& og = g.oct[o];
+            og.span = (int)(((long long)og.rows * og.gpr + nblk - 1) / nblk);
+            if (o > 0) rest += og.span;
+        }
+        if (nblk * g.batch >= (1ll << 31) || rest >= (1ll << 31))
+            return c->status(GDP_ERR_ARG, "image/batch too large for one context (split the batch)");
+        g.span_rest = (int)rest;
+        g.F = g.O;
+        g.tail_groups_per_img = 0;
+        g.tail_units = 0;
+        g.tiles_r = (int)nblk;
+        g.tiles_c = 1;
+        g.tiles_per_img = (unsigned)nblk;
+        g.tiles_total = (unsigned)(nblk * g.batch);
+        return GDP_OK;
+    }
     // octaves fused into a tile: those with whole rows in it (tile_rows = 2^(F-1)); the rest are
     // flattened tail units
     int fused = 1;

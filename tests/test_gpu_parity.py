@@ -147,11 +147,14 @@ def test_build_matches_oracle_shapes(pkg, oracle, H, W, S, O):
     _assert_same(_gpu_pyramid(pkg, img, S, O), want, (H, W, S, O))
 
 
-@pytest.mark.parametrize("variant", range(19))
+@pytest.mark.parametrize("variant", range(25))
 def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
-    """Every code variant of the build kernel (block size / tile width / octave-0 path, also
-    persistent grids and plain stores) produces identical bits."""
-    for H, W, S, O in [(100, 300, 2, 0), (67, 1000, 3, 5), (256, 512, 2, 9), (33, 65, 1, 0), (128, 1024, 2, 5)]:
+    """Every code variant of the build kernel (block size / tile width / octave-0 path, the
+    contiguous-span units of variants 19-24, also persistent grids and plain stores) produces
+    identical bits — including widths that are not a multiple of 4 (spans then cut inside a row's
+    ragged last group) and row bands."""
+    for H, W, S, O in [(100, 300, 2, 0), (67, 1000, 3, 5), (256, 512, 2, 9), (33, 65, 1, 0), (128, 1024, 2, 5),
+                       (270, 1918, 2, 5), (7, 3, 0, 0)]:
         img = oracle.lcg_image(H, W, 77 + variant)
         want = oracle.build_pyramid(img, S, O or None)
         with pkg.PyramidContext(H, W, S=S, octaves=O) as ctx:
@@ -161,6 +164,21 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
                 ctx.set_tuning(**kw)
                 ctx.build()
                 _assert_same(ctx.pyramid(0), want, (variant, H, W, S, O, kw))
+    # a row band of a 1080 x 1920 batch (config 3's shape) and of a tall image
+    for H, W, r0, r1, B in [(1080, 1920, 32, 544, 2), (4096, 256, 1024, 2048, 1)]:
+        imgs = [oracle.lcg_image(H, W, 5 + b) for b in range(B)]
+        with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B, row_begin=r0, row_end=r1) as ctx:
+            for b, im in enumerate(imgs):
+                ctx.set_input(im[r0:r1], b)
+            ctx.set_tuning(variant=variant, tile_order=1)
+            ctx.build()
+            for b, im in enumerate(imgs):
+                want = oracle.build_pyramid(im, 2, 5)
+                for o in range(5):
+                    rows, cols, first = ctx.level_dims(o)
+                    for s in range(5):
+                        lv = oracle.levels(want, H, W, 2, 5)[(o, s)][first:first + rows]
+                        _assert_same(ctx.level(b, o, s), lv, ("band", variant, H, W, r0, r1, b, o, s))
 
 
 def test_default_variant_follows_geometry(pkg):
@@ -174,7 +192,7 @@ def test_autotune_keeps_results_bit_exact(pkg, oracle):
     with pkg.PyramidContext(300, 512, S=2, octaves=5) as ctx:
         ctx.set_input(img)
         v, o, ms = ctx.autotune(iters=2)
-        assert 0 <= v <= 18 and o in (0, 1) and ms > 0
+        assert 0 <= v <= 24 and o in (0, 1) and ms > 0
         assert ctx.tuning()["variant"] == v and ctx.tuning()["tile_order"] == o
         ctx.build()
         _assert_same(ctx.pyramid(0), oracle.build_pyramid(img, 2, 5), ("autotuned", v, o))
