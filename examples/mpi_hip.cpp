@@ -3,7 +3,8 @@
 // Launch with any MPI: `mpiexec -n <ranks> examples/mpi_hip` (one GPU per rank), or directly
 // (MPI singleton, one rank).  Parity mode: mpi_hip [n] [lcg:SEED|ones] [dump.f32] [calls] [mixed]
 // — `calls` GenerateDoG_mpi calls on the same object (default 1); with "mixed" a single-process
-// GenerateDoG() runs between consecutive GenerateDoG_mpi calls.
+// GenerateDoG() runs between consecutive GenerateDoG_mpi calls; with "edit" the collector edits its
+// GaussPy between them (level (0, 1) zeroed, row 3 of level (0, 0) scaled by -2: two-way state).
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -35,8 +36,14 @@ int main(int argc, char* argv[]) {
     if (argc > 3) {  // parity mode: collective builds, the collector dumps its GaussPy
         const int calls = argc > 4 ? std::atoi(argv[4]) : 1;
         const bool mixed = argc > 5 && std::string(argv[5]) == "mixed";
+        const bool edit = argc > 5 && std::string(argv[5]) == "edit";
         for (int c = 0; c < calls; ++c) {
             if (c > 0 && mixed) g.GenerateDoG();
+            if (c > 0 && edit && g.rank() == 0) {
+                for (int r = 0; r < n; ++r)
+                    for (int k = 0; k < n; ++k) g.GaussPy[0][1][r][k] = 0.0f;
+                for (int k = 0; k < n; ++k) g.GaussPy[0][0][3][k] *= -2.0f;
+            }
             g.GenerateDoG_mgpu(argc, argv);  // = GenerateDoG_mpi (the SURVEY's name for the RCCL form)
         }
         if (g.rank() == 0) {

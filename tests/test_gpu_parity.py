@@ -875,6 +875,16 @@ def test_cpp_mpi_variant_dropin_collector(oracle, golden, tmp_path):
                 oracle.generate_dog(want, n, n, S, O)  # single-process GenerateDoG: serial centre
             oracle.generate_dog(want, n, n, S, O, centre="intlen")
         _assert_same(np.fromfile(out, dtype=np.float32), want, ("mpi re-entry", calls, mode))
+    for calls in (2, 3):  # the collector's GaussPy edited between calls is what the next call processes
+        subprocess.run([exe, str(n), spec, str(out), str(calls), "edit"], check=True, timeout=180, capture_output=True)
+        want = oracle.init_pyramid(img, S)
+        lv = oracle.levels(want, n, n, S, O)
+        for c in range(calls):
+            if c > 0:
+                lv[(0, 1)][:] = 0
+                lv[(0, 0)][3] *= np.float32(-2)
+            oracle.generate_dog(want, n, n, S, O, centre="intlen")
+        _assert_same(np.fromfile(out, dtype=np.float32), want, ("mpi host edits", calls))
 
 
 def test_reference_drivers_run_on_the_dropin(tmp_path):
