@@ -127,6 +127,11 @@ int gdp_gauss_octave(gdp_ctx* ctx, int octave, void* stream);
 /* GaussFilter(o) for every o in [o_begin, o_end) in ONE launch (the reference calls it per octave
  * from GenerateDoG, :139); the "row + column window pass" the north star's roofline target names. */
 int gdp_gauss_range(gdp_ctx* ctx, int o_begin, int o_end, void* stream);
+/* The window multiply of scales [s_begin, s_end) only, for every octave in [o_begin, o_end), in
+ * ONE launch: what worker rank i of the reference's MPI variant does to its own scale i before
+ * sending it to the collector (GaussPyramid_mpi::GenerateDoG_mpi, GaussDePyramid-MPI.h:271-290;
+ * its integer-length centre is GDP_CENTRE_INTLEN).  gdp_gauss_range is s = [0, S+3). */
+int gdp_gauss_scales(gdp_ctx* ctx, int s_begin, int s_end, int o_begin, int o_end, void* stream);
 /* DoG of octave o in place: level s -= level s+1 for s = 0..S+1 ascending
  * (GuassDePyramid.h:140-146). */
 int gdp_dog_octave(gdp_ctx* ctx, int octave, void* stream);

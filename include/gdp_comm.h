@@ -64,6 +64,28 @@ const char* gdp_comm_last_error(const gdp_comm* comm); /* comm may be NULL: last
 int gdp_comm_gather_bands(gdp_comm* comm, gdp_ctx* band, int band_image, gdp_ctx* full, int full_image, int root,
                           void* stream);
 
+/* ---- the reference's own role map (GaussPyramid_mpi::GenerateDoG_mpi, GaussDePyramid-MPI.h:265-335)
+ * Ranks i < S+3 ("workers") window scale i of every octave of their OWN pyramid and send it, level
+ * by level, to rank S+3 (the collector), which receives scale j from worker j and forms every DoG
+ * level; ranks > S+3 take no part.  Needs nranks >= S+4, as the reference does.  The drop-in class
+ * uses it when the world is that large (GaussDePyramid-HIP-mpi.h), leaving every rank's GaussPy
+ * where the reference leaves it: worker i with scale i windowed, the collector with the pyramid.
+ * gdp_comm_scale_plan: rank `rank`'s transfers (pure host arithmetic): a worker's sends (octave
+ * order), the collector's receives (worker-major, then octave: RCCL matches one peer pair's
+ * transfers in order), nothing for the others; GDP_ERR_ARG when nranks < S+4. */
+enum { GDP_SCALE_SEND = 0, GDP_SCALE_RECV = 1 };
+typedef struct gdp_scale_transfer {
+    int kind, peer, octave, scale;
+} gdp_scale_transfer;
+int gdp_comm_scale_plan(int S, int octaves, int nranks, int rank, gdp_scale_transfer* out, int capacity, int* count);
+/* Collective over the ranks of `comm` (>= S+4): executes gdp_comm_scale_plan on `ctx`, a
+ * whole-image context of the same geometry on every rank, image `image`: a worker's level
+ * (o, rank) goes to the collector's level (o, rank), whole levels, RCCL point-to-point in one
+ * group.  The window multiply (gdp_gauss_scales) before and the collector's DoG pass
+ * (gdp_dog_range) after are the caller's.  Stream-ordered on `stream` (NULL = the context's
+ * stream); blocking until the transfers are complete on return. */
+int gdp_comm_collect_scales(gdp_comm* comm, gdp_ctx* ctx, int image, void* stream);
+
 /* ---- halo exchange of the convolution extension on row bands (gdp_build_gaussian) ----------
  * The one step of the path with a real exchange: a band's convolution reads up to 6 * 2^(O-1)
  * input rows of each neighbouring band (gdp_conv_halo_rows).  Rank r sends its first rows to

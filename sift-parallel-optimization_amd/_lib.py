@@ -73,6 +73,7 @@ SIGNATURES = {
     "gdp_init": (_c_int, [_p, _p]),
     "gdp_gauss_octave": (_c_int, [_p, _c_int, _p]),
     "gdp_gauss_range": (_c_int, [_p, _c_int, _c_int, _p]),
+    "gdp_gauss_scales": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _p]),
     "gdp_dog_octave": (_c_int, [_p, _c_int, _p]),
     "gdp_dog_range": (_c_int, [_p, _c_int, _c_int, _p]),
     "gdp_generate_dog": (_c_int, [_p, _p]),

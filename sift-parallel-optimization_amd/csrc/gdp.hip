@@ -234,16 +234,17 @@ int launch_build(gdp_ctx* c, hipStream_t st, bool subset = false) {
 }
 
 template <int MODE, int SUB>
-int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st) {
+int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st, int sb = 0, int se = -1) {
     const Geom& g = c->geom;
     if constexpr (MODE == 1) {
-        const long long grid = ((long long)g.lv_blk[oe] - g.lv_blk[ob]) * g.L * g.batch * SUB;
+        const int Ls = (se < 0 ? g.L : se) - sb;  // scales [sb, sb + Ls) (gdp_gauss_scales), all by default
+        const long long grid = ((long long)g.lv_blk[oe] - g.lv_blk[ob]) * Ls * g.batch * SUB;
         if (grid <= 0) return GDP_OK;
         if (grid >= (1ll << 31) || (long long)g.lv_blk[g.O] * g.L >= (1ll << 32))
             return c->status(GDP_ERR_ARG, "window pass too large for one launch");
         auto wkern = c->nontemporal ? k_window<true, SUB> : k_window<false, SUB>;
         hipLaunchKernelGGL(wkern, dim3((unsigned)grid), dim3(kLevBlock / SUB), 0, st, c->d_geom, c->d_out, c->d_taps, ob,
-                           oe);
+                           oe, sb, Ls);
         GDP_HIP(c, hipGetLastError());
         return GDP_OK;
     }
@@ -262,7 +263,7 @@ int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st) {
 }
 
 template <int MODE>
-int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
+int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st, int sb = 0, int se = -1) {
     const Geom& g = c->geom;
     if ((MODE == 2 || MODE == 3) && c->inplace_sub == 0 && g.L <= 16) {
         const long long grid = ((long long)g.lx_blk[oe] - g.lx_blk[ob]) * g.batch;
@@ -274,11 +275,11 @@ int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st) {
         return GDP_OK;
     }
     switch (MODE == 1 ? c->window_sub : c->inplace_sub) {
-        case 2: return launch_inplace_sub<MODE, 2>(c, ob, oe, st);
-        case 4: return launch_inplace_sub<MODE, 4>(c, ob, oe, st);
-        case 8: return launch_inplace_sub<MODE, 8>(c, ob, oe, st);
-        case 16: return launch_inplace_sub<MODE, 16>(c, ob, oe, st);
-        default: return launch_inplace_sub<MODE, 1>(c, ob, oe, st);
+        case 2: return launch_inplace_sub<MODE, 2>(c, ob, oe, st, sb, se);
+        case 4: return launch_inplace_sub<MODE, 4>(c, ob, oe, st, sb, se);
+        case 8: return launch_inplace_sub<MODE, 8>(c, ob, oe, st, sb, se);
+        case 16: return launch_inplace_sub<MODE, 16>(c, ob, oe, st, sb, se);
+        default: return launch_inplace_sub<MODE, 1>(c, ob, oe, st, sb, se);
     }
 }
 
@@ -1147,6 +1148,13 @@ int gdp_gauss_range(gdp_ctx* c, int ob, int oe, void* stream) try {
     if (!c || ob < 0 || oe > c->geom.O || ob >= oe) return c ? c->status(GDP_ERR_ARG, "octave range invalid") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
     return launch_inplace<1>(c, ob, oe, c->pick(stream));
+} GDP_ABI_CATCH(c)
+
+int gdp_gauss_scales(gdp_ctx* c, int sb, int se, int ob, int oe, void* stream) try {
+    if (!c || ob < 0 || oe > c->geom.O || ob >= oe || sb < 0 || se > c->geom.L || sb >= se)
+        return c ? c->status(GDP_ERR_ARG, "gdp_gauss_scales: scale / octave range invalid") : GDP_ERR_ARG;
+    GDP_HIP(c, hipSetDevice(c->device));
+    return launch_inplace<1>(c, ob, oe, c->pick(stream), sb, se);
 } GDP_ABI_CATCH(c)
 
 int gdp_dog_octave(gdp_ctx* c, int o, void* stream) try {

@@ -78,6 +78,20 @@ std::vector<gdp_transfer> make_plan(int H, int W, int S, int O, int nranks, int 
     return plan;
 }
 
+// The reference's role map (gdp_comm_scale_plan): worker i < L sends level (o, i) of every octave
+// to collector L; the collector receives worker-major, then octave.
+int make_scale_plan(int S, int O, int nranks, int rank, std::vector<gdp_scale_transfer>& plan) {
+    const int L = S + 3;
+    if (nranks < L + 1) return GDP_ERR_ARG;
+    if (rank < L) {
+        for (int o = 0; o < O; ++o) plan.push_back({GDP_SCALE_SEND, L, o, rank});
+    } else if (rank == L) {
+        for (int j = 0; j < L; ++j)
+            for (int o = 0; o < O; ++o) plan.push_back({GDP_SCALE_RECV, j, o, j});
+    }
+    return GDP_OK;
+}
+
 // The halo exchange schedule (gdp_comm_halo_plan): rows a band's convolution reads beyond it are
 // 6 * 2^(O-1) clipped to the image (gdp_conv_halo_rows), exchanged with the adjacent bands.
 int halo_counts_side(int H, int O, int r0, int r1, int side) {
@@ -237,6 +251,49 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
         GDP_HIPC(c, hipMemcpyAsync(dst, gdp_device_level(band, band_image, t.octave, t.scale),
                                    (size_t)t.rows * t.cols * 4, hipMemcpyDeviceToDevice, st));
     }
+    GDP_HIPC(c, hipStreamSynchronize(st));
+    return GDP_OK;
+} GDP_COMM_CATCH(c)
+
+int gdp_comm_scale_plan(int S, int O, int nranks, int rank, gdp_scale_transfer* out, int capacity, int* count) try {
+    if (S < 0 || O <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || !count || capacity < 0 || (capacity > 0 && !out))
+        return fail(nullptr, GDP_ERR_ARG, "gdp_comm_scale_plan: bad argument");
+    std::vector<gdp_scale_transfer> plan;
+    if (make_scale_plan(S, O, nranks, rank, plan) != GDP_OK)
+        return fail(nullptr, GDP_ERR_ARG, "gdp_comm_scale_plan: the reference's role map needs >= S+4 ranks");
+    *count = (int)plan.size();
+    if ((int)plan.size() > capacity) return fail(nullptr, GDP_ERR_ARG, "gdp_comm_scale_plan: capacity too small");
+    std::copy(plan.begin(), plan.end(), out);
+    return GDP_OK;
+} GDP_COMM_CATCH(nullptr)
+
+int gdp_comm_collect_scales(gdp_comm* c, gdp_ctx* ctx, int image, void* stream) try {
+    if (!c || !ctx) return fail(c, GDP_ERR_ARG, "gdp_comm_collect_scales: bad argument");
+    int H, W, S, O, B;
+    if (gdp_get_geometry(ctx, &H, &W, &S, &O, &B) != GDP_OK || image < 0 || image >= B)
+        return fail(c, GDP_ERR_ARG, "gdp_comm_collect_scales: bad context / image");
+    int rows0, cols0, first0;
+    gdp_level_dims(ctx, 0, &rows0, &cols0, &first0);
+    if (first0 != 0 || rows0 != H) return fail(c, GDP_ERR_ARG, "gdp_comm_collect_scales needs a whole-image context");
+    std::vector<gdp_scale_transfer> plan;
+    if (make_scale_plan(S, O, c->nranks, c->rank, plan) != GDP_OK)
+        return fail(c, GDP_ERR_ARG, "gdp_comm_collect_scales: the reference's role map needs >= S+4 ranks");
+    if (plan.empty()) return GDP_OK;  // ranks > S+3 take no part (GaussDePyramid-MPI.h:269-335)
+    GDP_HIPC(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)gdp_stream(ctx);
+    GDP_NCCL(c, ncclGroupStart());
+    for (const gdp_scale_transfer& t : plan) {
+        int rows, cols, first;
+        gdp_level_dims(ctx, t.octave, &rows, &cols, &first);
+        const size_t n = (size_t)rows * cols;
+        if (n == 0) continue;
+        float* lev = const_cast<float*>(gdp_device_level(ctx, image, t.octave, t.scale));
+        if (t.kind == GDP_SCALE_SEND)
+            GDP_NCCL(c, ncclSend(lev, n, ncclFloat, t.peer, c->comm, st));
+        else
+            GDP_NCCL(c, ncclRecv(lev, n, ncclFloat, t.peer, c->comm, st));
+    }
+    GDP_NCCL(c, ncclGroupEnd());
     GDP_HIPC(c, hipStreamSynchronize(st));
     return GDP_OK;
 } GDP_COMM_CATCH(c)

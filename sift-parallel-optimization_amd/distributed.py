@@ -253,7 +253,24 @@ def assemble_bands(H, W, S, octaves, world, packed_bands, like=None):
     return full
 
 
-def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None, centre="serial"):
+def scale_plan(S, octaves, world, rank):
+    """The reference's role map (GaussPyramid_mpi::GenerateDoG_mpi, GaussDePyramid-MPI.h:265-335) on
+    `rank`: [(kind, peer, octave, scale)] — worker i < S+3 sends level (o, i) of every octave to the
+    collector S+3 (octave order, :285); the collector receives worker-major, then octave (:295-303);
+    ranks > S+3 take no part.  Needs world >= S+4 (the reference's own requirement).  Equals
+    libgdp_comm's gdp_comm_scale_plan."""
+    L = int(S) + 3
+    if world < L + 1:
+        raise ValueError(f"the reference's role map needs >= S+4 = {L + 1} ranks, world is {world}")
+    if rank < L:
+        return [("send", L, o, rank) for o in range(octaves)]
+    if rank == L:
+        return [("recv", j, o, j) for j in range(L) for o in range(octaves)]
+    return []
+
+
+def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None, centre="serial", roles="bands",
+                      scale_compute=None, collect=None):
     """Collector semantics of GenerateDoG_mpi (GaussDePyramid-MPI.h:265-335) over RCCL.
 
     Every rank passes the same `img` (the reference also replicates the input on every rank,
@@ -263,8 +280,20 @@ def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None
     injected (tests use it to run this logic under gloo on CPU); by default it is the HIP build.
     `centre="intlen"` reproduces the MPI variant's own window centre (GaussDePyramid-MPI.h:273;
     differs from the serial header only when n is not a multiple of 2^(octaves-1)).
+
+    roles="reference" runs the reference's own role map instead (scale_plan; world >= S+4): worker
+    i windows scale i of every octave of its pyramid with the variant's integer-length centre
+    (`scale_compute(img, i) -> [O flat float32 tensors]`, default: a libgdp context's
+    gdp_gauss_scales), sends it to the collector S+3, which forms every DoG level
+    (`collect(levels[j][o]) -> packed pyramid`, default: the collector's context, gdp_dog_range)
+    and returns the pyramid; every other rank returns None.
     """
     import torch
+
+    if roles == "reference":
+        return _generate_dog_roles(img, n, S, octaves, dist, device, scale_compute, collect)
+    if roles != "bands":
+        raise ValueError(f"roles must be 'bands' or 'reference', not {roles!r}")
 
     world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
@@ -281,6 +310,78 @@ def generate_dog_mgpu(img, n, S, octaves=0, dist=None, compute=None, device=None
     if rank != 0:
         return None
     return assemble_bands(n, n, S, O, world, bands)
+
+
+def _generate_dog_roles(img, n, S, octaves, dist, device, scale_compute, collect):
+    """generate_dog_mgpu(roles="reference"): the reference's scale split over point-to-point
+    transfers (RCCL over xGMI under "nccl", gloo in CPU tests)."""
+    import torch
+
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    O = octaves or octaves_for(n)
+    L = S + 3
+    plan = scale_plan(S, O, world, rank)  # raises below S+4 ranks, as the reference cannot run either
+    img = np.ascontiguousarray(np.asarray(img, dtype=np.int32)[:n, :n])
+    sizes = [(n >> o) * (n >> o) for o in range(O)]
+    if scale_compute is None or collect is None:
+        dflt_scale, dflt_collect = _gpu_role_compute(n, S, O, device)
+        scale_compute, collect = scale_compute or dflt_scale, collect or dflt_collect
+    if rank < L:
+        levels = scale_compute(img, rank)  # GaussDePyramid-MPI.h:271-284: window this rank's scale
+        ops = [dist.P2POp(dist.isend, levels[o].contiguous(), peer) for kind, peer, o, _ in plan]
+    elif rank == L:
+        dev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
+        recv = [[torch.empty(sizes[o], dtype=torch.float32, device=dev) for o in range(O)] for _ in range(L)]
+        ops = [dist.P2POp(dist.irecv, recv[j][o], peer) for kind, peer, o, j in plan]
+    else:
+        return None  # ranks > S+3 take no part (:269-335)
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    if rank != L:
+        return None
+    return collect(recv)  # :304-318: every DoG level on the collector
+
+
+def _gpu_role_compute(n, S, O, device):
+    """Default worker / collector steps of the reference role map on a libgdp whole-image context
+    (integer-length window centre, GaussDePyramid-MPI.h:273)."""
+    import torch
+
+    from .gausspyramid import PyramidContext
+
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+
+    def bound_ctx():
+        ctx = PyramidContext(n, n, S=S, octaves=O, batch=1, device=dev.index, centre="intlen")
+        out = torch.empty(ctx.pyramid_bytes() // 4 + 64, dtype=torch.float32, device=dev)
+        shift = (-out.data_ptr() % 256) // 4
+        view = out[shift:shift + ctx.pyramid_bytes() // 4]
+        ctx.bind_device_output(view.data_ptr(), ctx.pyramid_bytes(), keepalive=out)
+        return ctx, view
+
+    def levels_of(ctx, view, s):
+        return [view[ctx.level_offset(0, o, s):ctx.level_offset(0, o, s) + (n >> o) * (n >> o)] for o in range(O)]
+
+    def scale_compute(img, i):
+        ctx, view = bound_ctx()
+        ctx.set_input(img)
+        ctx.init()                              # GaussPyInit (the constructor's state)
+        ctx.gauss_scales(i, i + 1)              # this worker's scale, every octave
+        ctx.sync()
+        return levels_of(ctx, view, i)
+
+    def collect(recv):
+        ctx, view = bound_ctx()
+        for j in range(S + 3):
+            for o, dst in enumerate(levels_of(ctx, view, j)):
+                dst.copy_(recv[j][o])
+        torch.cuda.current_stream(dev).synchronize()
+        ctx.dog_range(0, O)
+        ctx.sync()
+        return torch.cat([lv for o in range(O) for s in range(S + 3) for lv in [levels_of(ctx, view, s)[o]]])
+
+    return scale_compute, collect
 
 
 def _gpu_band_compute(H, W, S, O, device, centre="serial"):

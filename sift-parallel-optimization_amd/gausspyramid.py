@@ -221,6 +221,13 @@ class PyramidContext:
         o_end = self.O if o_end is None else o_end
         check(lib().gdp_gauss_range(self._ctx, int(o_begin), int(o_end), _stream_handle(stream)), self._ctx)
 
+    def gauss_scales(self, s_begin, s_end, o_begin=0, o_end=None, stream=None):
+        """Window multiply of scales [s_begin, s_end) of octaves [o_begin, o_end) in place (the MPI
+        variant's worker step, GaussDePyramid-MPI.h:271-290)."""
+        o_end = self.O if o_end is None else o_end
+        check(lib().gdp_gauss_scales(self._ctx, int(s_begin), int(s_end), int(o_begin), int(o_end),
+                                     _stream_handle(stream)), self._ctx)
+
     def dog_octave(self, o, stream=None):
         check(lib().gdp_dog_octave(self._ctx, int(o), _stream_handle(stream)), self._ctx)
 

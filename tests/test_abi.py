@@ -110,7 +110,7 @@ def test_comm_library_exports_its_header(pkg):
     pkg.lib()  # torch first, then libgdp (the comm library links both)
     L = _comm_lib()
     names = pkg.header_functions(os.path.join(REPO, "include", "gdp_comm.h"))
-    assert len(names) == 11
+    assert len(names) == 13
     for n in names:
         assert hasattr(L, n), n
 
