@@ -39,14 +39,14 @@ int main(int argc, char* argv[]) {
         const bool edit = argc > 5 && std::string(argv[5]) == "edit";
         for (int c = 0; c < calls; ++c) {
             if (c > 0 && mixed) g.GenerateDoG();
-            if (c > 0 && edit && g.rank() == 0) {
+            if (c > 0 && edit && g.rank() == g.collector()) {
                 for (int r = 0; r < n; ++r)
                     for (int k = 0; k < n; ++k) g.GaussPy[0][1][r][k] = 0.0f;
                 for (int k = 0; k < n; ++k) g.GaussPy[0][0][3][k] *= -2.0f;
             }
             g.GenerateDoG_mgpu(argc, argv);  // = GenerateDoG_mpi (the SURVEY's name for the RCCL form)
         }
-        if (g.rank() == 0) {
+        if (g.rank() == g.collector()) {  // rank 0, or S+3 under the reference's role map (>= S+4 ranks)
             FILE* f = std::fopen(argv[3], "wb");
             for (int o = 0, len = n; len; ++o, len /= 2)
                 for (int sc = 0; sc < 5; ++sc)
@@ -65,6 +65,6 @@ int main(int argc, char* argv[]) {
         elapsed += end - start;
         times += 1;
     }
-    if (g.rank() == 0) std::printf("%g ms/call (collector, incl. gather + GaussPy host mirror)\n", elapsed.count() / times);
+    if (g.rank() == g.collector()) std::printf("%g ms/call (collector, incl. gather + GaussPy host mirror)\n", elapsed.count() / times);
     return 0;
 }

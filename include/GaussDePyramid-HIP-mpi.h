@@ -38,6 +38,14 @@
 // live in its band context), so it uploads only when the caller sets `host_dirty`.  In the
 // reference the collector's output depends only on the workers' states (scale i from rank i); here
 // on every rank's own rows — the same whenever the ranks hold the same GaussPy (SPMD callers).
+// Role map: with >= S+4 ranks (the reference's own requirement) the class reproduces the
+// reference's roles by default (`roles = ROLES_AUTO`; ROLES_REFERENCE forces them, ROLES_BANDS the
+// band split): rank i < S+3 windows scale i of every octave of its own state (gdp_gauss_scales,
+// integer-length centre) and sends it to rank S+3 (gdp_comm_collect_scales), which forms every DoG
+// level (gdp_dog_range); ranks > S+3 take no part.  Every rank's GaussPy then ends where the
+// reference leaves it: worker i with scale i windowed (the other scales untouched), the collector
+// (collector() == S+3) with the pyramid.  With fewer ranks the band split above runs and the
+// collector is rank 0.
 // Differences: MPI is initialised once (if the caller has not) and finalised by the
 // destructor, so GenerateDoG_mpi may be called repeatedly (the reference calls
 // MPI_Init/MPI_Finalize inside and cannot); errors abort with a message instead of continuing.
@@ -79,6 +87,9 @@ public:
     int chunk_size;
     int all_time;
     int rank() const { return rank_; }
+    enum { ROLES_AUTO = 0, ROLES_BANDS = 1, ROLES_REFERENCE = 2 };
+    int roles = ROLES_AUTO;  // see the header comment; decided at the first GenerateDoG_mpi
+    int collector() const { return ref_roles_ ? S + 3 : 0; }  // the rank holding the pyramid
     bool mirror_host = true;  // two-way GaussPy (see the header comment)
     bool host_dirty = false;  // the caller edited GaussPy / data: upload before the next call
     void SyncHost() { sync_host_(); host_current_ = true; }
@@ -98,6 +109,8 @@ protected:
     bool fresh_;      // contents == GaussPyInit() on every rank
     bool band_live_;  // band_ holds this rank's rows of the last GenerateDoG_mpi result
     bool host_current_ = true;  // GaussPy mirrors full_ (false on workers after GenerateDoG_mpi)
+    bool ref_roles_ = false;    // the reference's role map is in use (>= S+4 ranks)
+    bool band_tried_ = false;   // the band context was planned (band split only)
     bool rows_in_mirror_() const {
         if (!host_) return false;
         for (int o = 0; o < layer; ++o)
@@ -250,6 +263,35 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
         if (rank_ == 0) check_comm_(gdp_comm_unique_id(id), "GenerateDoG_mpi", nullptr);
         MPI_Bcast(id, GDP_COMM_ID_BYTES, MPI_BYTE, 0, MPI_COMM_WORLD);
         check_comm_(gdp_comm_init(&comm_, id, size_, rank_, device), "GenerateDoG_mpi", nullptr);
+        if (roles == ROLES_REFERENCE && size_ < S + 4) {
+            std::fprintf(stderr, "GaussPyramid_hip_mpi: the reference's role map needs >= S+4 = %d ranks, have %d\n",
+                         S + 4, size_);
+            std::abort();
+        }
+        ref_roles_ = roles == ROLES_REFERENCE || (roles == ROLES_AUTO && size_ >= S + 4);
+    }
+    if (ref_roles_) {  // GaussDePyramid-MPI.h:265-335, role for role
+        pull_host_();
+        const int L = S + 3;
+        if (rank_ < L) {  // worker: window this rank's scale of every octave (:271-284)
+            check_(gdp_set_window_centre(full_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi", full_);
+            const int rc = gdp_gauss_scales(full_, rank_, rank_ + 1, 0, layer, nullptr);
+            check_(gdp_set_window_centre(full_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi", full_);
+            check_(rc, "GenerateDoG_mpi", full_);
+        }
+        // worker scale i -> collector level (o, i) (:285 / :295-303)
+        check_comm_(gdp_comm_collect_scales(comm_, full_, 0, nullptr), "GenerateDoG_mpi", comm_);
+        if (rank_ == L) check_(gdp_dog_range(full_, 0, layer, nullptr), "GenerateDoG_mpi", full_);  // :304-318
+        check_(gdp_sync(full_), "GenerateDoG_mpi", full_);
+        fresh_ = band_live_ = false;
+        if (rank_ <= L) {
+            if (mirror_host) SyncHost();
+            else host_current_ = false;
+        }
+        return;
+    }
+    if (!band_ && !band_tried_) {
+        band_tried_ = true;
         int r0, r1;
         check_comm_(gdp_band_rows(length, size_, rank_, layer, &r0, &r1), "GenerateDoG_mpi", nullptr);
         if (r1 > r0) {  // more ranks than aligned bands leaves the last ranks without rows

@@ -227,3 +227,40 @@ def test_inplace_zero_window_is_exact_for_caller_values_near_flt_max(pkg, oracle
                 ctx.sync()
                 _assert_same_nan(ctx.pyramid(0), oracle.generate_dog(base.copy(), n, n, S, O), ("regen", zw, sub))
     assert np.isnan(lv(oracle.gauss_octave(base.copy(), n, n, S, 0), 0, S + 2)[0, c])  # the case exists
+
+
+def test_reference_role_map_steps_on_the_gpu(pkg, oracle):
+    """The reference's role map (GaussDePyramid-MPI.h:265-335), its two device steps on one GPU:
+    each worker's gdp_gauss_scales(i, i+1) of its own pyramid (integer-length centre) == the
+    worker state the reference leaves (scale i windowed, the others at GaussPyInit values), and the
+    collector's DoG pass over the S+3 workers' scales == the reference collector's pyramid
+    (tests/golden/mpi_hashes.json).  The RCCL transport between them (gdp_comm_collect_scales) needs
+    >= S+4 GPUs; its schedule is tested on CPU (tests/test_distributed.py)."""
+    import importlib
+    import json
+
+    import torch
+
+    d = importlib.import_module(pkg.__name__ + ".distributed")
+    with open(os.path.join(REPO, "tests", "golden", "mpi_hashes.json")) as f:
+        recs = [r for r in json.load(f) if r["variant"] == "GaussDePyramid-MPI.h:GenerateDoG_mpi"]
+    for rec in recs:
+        n, S, spec = rec["n"], rec["S"], rec["input"]
+        O = oracle.octaves(n)
+        img = oracle.image_from_spec(n, spec)
+        scale_compute, collect = d._gpu_role_compute(n, S, O, 0)
+        init = oracle.levels(oracle.init_pyramid(img, S), n, n, S, O)
+        scales = []
+        for i in range(S + 3):
+            lv = scale_compute(img, i)
+            for o in range(O):  # the worker's own scale: (x * fc) * fr with the variant's centre
+                fc = oracle.taps(n, o, i, centre="intlen")
+                want = (init[(o, i)] * fc[None, :]) * fc[:, None]
+                _assert_same(lv[o].cpu().numpy(), want.astype(np.float32).ravel(), ("worker", n, i, o))
+            scales.append([t.clone() for t in lv])
+        got = collect(scales).cpu().numpy()
+        lvs = oracle.levels(got, n, n, S, O)
+        for o, row in enumerate(rec["octaves"]):
+            for s, h in enumerate(row):
+                assert oracle.fnv(lvs[(o, s)]) == int(h, 16), ("collector", n, S, spec, o, s)
+        torch.cuda.synchronize()
