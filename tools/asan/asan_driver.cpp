@@ -71,6 +71,41 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
     std::vector<float> packed(gdp_packed_floats(c));
     OK(gdp_download_pyramid(c, 0, packed.data()));
     OK(gdp_upload_pyramid(c, 0, packed.data()));
+    {  // round 4: host -> device state (two-way GaussPy) — raw, row-pointer and per-level uploads
+        uint64_t before = 0, after = 0;
+        OK(gdp_checksum(c, 0, &before));
+        std::vector<float> raw(gdp_image_floats(c));
+        OK(gdp_download_image_raw(c, 0, raw.data()));
+        OK(gdp_upload_image_raw(c, 0, raw.data()));
+        std::vector<std::vector<std::vector<float>>> rows_store(go);
+        std::vector<std::vector<float*>> rowp(go * (gs + 3));
+        std::vector<float**> lev(go * (gs + 3));
+        std::vector<float***> oct(go);
+        for (int o = 0; o < go; ++o) {
+            int lr, lc, first;
+            OK(gdp_level_dims(c, o, &lr, &lc, &first));
+            for (int s = 0; s < gs + 3; ++s) {
+                std::vector<float*>& rp = rowp[o * (gs + 3) + s];
+                rows_store[o].emplace_back((size_t)lr * lc + 1);
+                for (int r = 0; r < lr; ++r) rp.push_back(rows_store[o].back().data() + (size_t)r * lc);
+                if (rp.empty()) rp.push_back(rows_store[o].back().data());
+                lev[o * (gs + 3) + s] = rp.data();
+            }
+            oct[o] = lev.data() + o * (gs + 3);
+        }
+        OK(gdp_download_pyramid_rows(c, 0, oct.data()));
+        OK(gdp_upload_pyramid_rows(c, 0, (const float* const* const* const*)oct.data()));
+        for (int o = 0; o < go; ++o)
+            for (int s = 0; s < gs + 3; ++s) {
+                OK(gdp_upload_level(c, 0, o, s, rows_store[o][s].data()));
+                OK(gdp_upload_level_rows(c, 0, o, s, rowp[o * (gs + 3) + s].data()));
+            }
+        OK(gdp_checksum(c, 0, &after));
+        EXPECT(before == after);
+        EXPECT(gdp_upload_level(c, 0, go, 0, raw.data()) == GDP_ERR_ARG);
+        OK(gdp_gauss_scales(c, 1, 2, 0, go, nullptr));
+        EXPECT(gdp_gauss_scales(c, 2, 2, 0, go, nullptr) == GDP_ERR_ARG);
+    }
     OK(gdp_gauss_range(c, 0, go, nullptr));
     // tuning: every key, valid and invalid values
     for (int key = 1; key <= 11; ++key) {
