@@ -20,7 +20,7 @@ def per_dispatch(d, counters):
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(p) as f:
             for r in csv.DictReader(f):
-                if r["Counter_Name"] in counters:
+                if r["Counter_Name"] in counters and ("k_b128" in r["Kernel_Name"] or "k_b32" in r["Kernel_Name"]):
                     rows.setdefault(int(r["Dispatch_Id"]), {})[r["Counter_Name"]] = float(r["Counter_Value"])
     return [rows[k] for k in sorted(rows)]
 
