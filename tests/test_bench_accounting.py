@@ -210,13 +210,23 @@ def test_traffic_records_match_only_their_kernel_instance():
     import bench
 
     for cfg in ("c2", "c3", "c4", "c5"):
-        for v in range(19):
+        for v in range(27):  # every variant the autotune can pick (19-26: contiguous spans, round 4)
             for t in (0, 1):
                 for zw in (0, 1):  # the autotune also picks GDP_TUNE_ZERO_WINDOW
                     rec = bench.latest_pmc(cfg, v, t, zero_window=zw)
                     assert rec is not None and rec["variant"] == v and rec["tile_order"] == t, (cfg, v, t, zw)
                     assert rec.get("zero_window", 0) == zw, (cfg, v, t, zw)
-                    assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
+                    assert rec.get("band_of") is None
+                    # spans in the linear order re-read neighbouring units' decimated rows (<= 1.11x)
+                    assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < \
+                        (1.12 if v >= 19 else 1.05), (cfg, v, t, zw)
+    for n in (2, 4, 8):  # config 5 at N > 1: rank 0's band of N
+        for v in range(27):
+            for t in (0, 1):
+                for zw in (0, 1):
+                    rec = bench.latest_pmc("c5", v, t, zero_window=zw, band_of=n)
+                    assert rec is not None and rec["band_of"] == n and rec["band_rows"][0] == 0, (n, v, t, zw)
+                    assert rec["algorithmic_bytes_per_launch"] < bench.algorithmic_bytes(16384, 16384, 2, 5, 1) / n * 1.01
     assert bench.latest_pmc("c2", 99, 0) is None
     conv = bench.latest_conv_pmc("c2", {"conv_kernel": 2, "conv_rows": 32, "conv_order": 4})
     assert conv is not None and conv["op"] == "conv"
