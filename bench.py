@@ -836,7 +836,9 @@ def main():
     local = local if backend == "nccl" else local % max(1, ndev)
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    # GDP_BENCH_FORCE_PG=1 (under torchrun --nproc-per-node 1): open the process group at N = 1 too,
+    # so a 1-GPU box exercises the RCCL init, barriers and object gathers the N > 1 line takes
+    if world > 1 or os.environ.get("GDP_BENCH_FORCE_PG") == "1":
         import torch.distributed as dist
 
         # self-launched ranks meet through a file (launch_ranks); under torchrun, env:// as usual
