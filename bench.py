@@ -1027,6 +1027,8 @@ def main():
     pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3,
                       tun["zero_window"] if args.op == "build" else 0, band_of=band_of)
            if args.op in ("build", "subset") and args.input == "i32" and (band_of is None or rank == 0) else None)
+    if os.environ.get("GDP_IMAGE_STRIDE_MB"):
+        pmc = None  # the PMC records are of the dense layout
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
     if args.op in ("regen", "gauss") and not (cfg["band"] and world > 1):
@@ -1053,6 +1055,12 @@ def main():
             "input_format": "int32" if args.input == "i32" else "uint8",
             "rotated_buffer_sets": rotate,
             "working_set_bytes_per_gpu": rotate * set_bytes,
+            **({"layout": {"GDP_IMAGE_STRIDE_MB": int(os.environ["GDP_IMAGE_STRIDE_MB"]),
+                           "note": "images spread out (DESIGN.md §5.1 XCD-range placement): same bytes moved, "
+                                   "larger allocation",
+                           "allocated_pyramid_bytes_per_set": (1 if cfg["band"] else B) * max(
+                               4 * (S + 3) * pyramid_pixels(H, W, O), int(os.environ["GDP_IMAGE_STRIDE_MB"]) << 20)}}
+               if os.environ.get("GDP_IMAGE_STRIDE_MB") else {}),
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

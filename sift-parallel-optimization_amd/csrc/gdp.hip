@@ -693,6 +693,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
     g.pyr_stride = round_up(lev_off, kLevelAlign);
+    // optional image stride (MiB) — layout experiment knob, like GDP_LEVEL_PAD: images that far
+    // apart, so tile order 1's eight XCD ranges (batch / 8 images each) start 8 x stride apart
+    if (const char* is_env = std::getenv("GDP_IMAGE_STRIDE_MB"))
+        g.pyr_stride = std::max(g.pyr_stride, round_up(std::max(0ll, std::atoll(is_env)) << 18, kLevelAlign));
     const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
     const long long tail_units = (tail_per_img * batch + kTailGroups - 1) / kTailGroups;
     const long long min_tiles = (long long)((g.in_rows + kTileRows - 1) / kTileRows) * ((W + 63) / 64) * batch;

@@ -181,6 +181,28 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
                         _assert_same(ctx.level(b, o, s), lv, ("band", variant, H, W, r0, r1, b, o, s))
 
 
+def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch):
+    """GDP_IMAGE_STRIDE_MB (the XCD-range placement experiment) only moves images
+    apart: every image, level and checksum equals the dense layout's, in both tile orders."""
+    H, W, B = 300, 500, 3
+    imgs = [oracle.lcg_image(H, W, 40 + b) for b in range(B)]
+    with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as dense:
+        for b, im in enumerate(imgs):
+            dense.set_input(im, b)
+        dense.build()
+        sums = [dense.checksum(b) for b in range(B)]
+    monkeypatch.setenv("GDP_IMAGE_STRIDE_MB", "3")
+    with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as ctx:
+        for b, im in enumerate(imgs):
+            ctx.set_input(im, b)
+        for order in (0, 1):
+            ctx.set_tuning(variant=0, tile_order=order)
+            ctx.build()
+            for b, im in enumerate(imgs):
+                _assert_same(ctx.pyramid(b), oracle.build_pyramid(im, 2, 5), ("stride", order, b))
+                assert ctx.checksum(b) == sums[b]
+
+
 def test_default_variant_follows_geometry(pkg):
     with pkg.PyramidContext(64, 4096, S=2, batch=2) as a, pkg.PyramidContext(64, 1920, S=2) as b, \
             pkg.PyramidContext(4096, 4096, S=2, octaves=5) as c:
