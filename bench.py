@@ -226,13 +226,15 @@ def latest_conv_pmc(config_key, tun):
     return best
 
 
-def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0, band_of=None):
+def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0, band_of=None,
+               image_stride_mb=None):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
     whose recorded build variant, tile order and zero-window mode equal the run's; None when no profile of that
     instance exists (the traffic of another variant would describe a different kernel).  band_of = N:
     the row-band config's per-rank launch at N ranks (rank 0's band of N, profiled on one GPU by
-    tools/pmc_variants.py --band-of N), not the whole image's."""
+    tools/pmc_variants.py --band-of N), not the whole image's.  image_stride_mb: the spread layout's
+    records (GDP_IMAGE_STRIDE_MB), kept apart from the dense layout's."""
     pdir = os.path.join(REPO, "profiles")
     best = None
     if os.path.isdir(pdir):
@@ -249,6 +251,7 @@ def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_windo
                         rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
                         rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32" and \
                         rec.get("zero_window", 0) == zero_window and rec.get("band_of") == band_of and \
+                        rec.get("image_stride_mb") == image_stride_mb and \
                         lt in rec.get("kernel", lt):
                     best = dict(rec, file=f)
     return best
@@ -769,6 +772,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="override images per GPU")
+    ap.add_argument("--image-stride-mb", type=int, default=None,
+                    help="spread layout: images this many MiB apart (GDP_IMAGE_STRIDE_MB; DESIGN.md §5.1)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None,
@@ -816,6 +821,8 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the N ranks here, before torch is imported or a GPU is touched
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.image_stride_mb:
+        os.environ["GDP_IMAGE_STRIDE_MB"] = str(args.image_stride_mb)  # read when each context is created
 
     import torch
 
@@ -1025,10 +1032,10 @@ def main():
     # launch, profiled separately as rank 0's band of N on one GPU (tools/pmc_variants.py --band-of N)
     band_of = world if (cfg["band"] and world > 1) else None
     pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3,
-                      tun["zero_window"] if args.op == "build" else 0, band_of=band_of)
+                      tun["zero_window"] if args.op == "build" else 0, band_of=band_of,
+                      image_stride_mb=int(os.environ["GDP_IMAGE_STRIDE_MB"]) if os.environ.get("GDP_IMAGE_STRIDE_MB")
+                      else None)
            if args.op in ("build", "subset") and args.input == "i32" and (band_of is None or rank == 0) else None)
-    if os.environ.get("GDP_IMAGE_STRIDE_MB"):
-        pmc = None  # the PMC records are of the dense layout
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
     if args.op in ("regen", "gauss") and not (cfg["band"] and world > 1):

@@ -86,6 +86,14 @@ void gdp_destroy(gdp_ctx* ctx);
 int gdp_get_geometry(const gdp_ctx* ctx, int* height, int* width, int* S, int* octaves, int* batch);
 int gdp_level_dims(const gdp_ctx* ctx, int octave, int* rows, int* cols, int* first_row);
 size_t gdp_pyramid_bytes(const gdp_ctx* ctx); /* device bytes of all pyramids of the batch */
+/* Layout knobs read from the environment when a context is created (experiments; every setting
+ * gives identical bits): GDP_LEVEL_PAD (floats between levels), GDP_ROWTAP_LAYOUT (non-square row
+ * windows [row][scale] = 1 / [scale][row] = 0), GDP_IMAGE_STRIDE_MB (images at least this many MiB
+ * apart: the "spread" layout of DESIGN.md §5.1, which lets tile order 1's eight XCD ranges of a
+ * batch lie gigabytes apart), GDP_SPREAD_VMM = 1 (the pyramid as a reserved address range with one
+ * physical chunk mapped per image; the gaps stay unmapped) with GDP_SPREAD_PHYS_MB (physical
+ * spacer created after each chunk and released once all are mapped).  gdp_pyramid_bytes and
+ * gdp_level_offset follow the spread stride; gdp_image_floats stays one image's dense extent. */
 
 /* ---- input ---------------------------------------------------------------------------------
  * The reference deep-copies `int** img` in its constructor (GuassDePyramid.h:38-46).  These
@@ -236,7 +244,8 @@ size_t gdp_level_offset(const gdp_ctx* ctx, int b, int octave, int scale);
  * gdp_host_alloc: pinned (page-locked) host memory, which one DMA copy fills at the full PCIe
  * rate (gdp_host_free releases it).  gdp_image_floats: floats of one image's pyramid in the device
  * layout — level (o, s) at gdp_level_offset(ctx, 0, o, s), dense rows of cols_o floats, levels
- * 256-B aligned.  gdp_download_image_raw: copy image b's pyramid in that layout to `host` in ONE
+ * 256-B aligned (the dense extent, also under a spread layout).  gdp_download_image_raw: copy
+ * image b's pyramid in that layout to `host` in ONE
  * D2H copy (blocking).  A caller that points the reference's float**** rows into such a buffer
  * (GaussPy[o][s][r] = host + gdp_level_offset(ctx, 0, o, s) + r * cols_o) mirrors the device with
  * no per-row scatter (include/GaussDePyramid-HIP.h does). */

@@ -113,6 +113,15 @@ struct gdp_ctx {
     bool conv_perm_dirty = true;
     int conv_perm_kernel = -1;       // the conv kernel d_conv_perm was built for (its block prefix)
     float* d_out_own = nullptr;   // context-owned pyramid (d_out may point at caller memory)
+    long long img_floats = 0;     // one image's dense extent (pyr_stride may be larger: GDP_IMAGE_STRIDE_MB)
+    // GDP_SPREAD_VMM: the pyramid as one reserved address range with separately created physical
+    // chunks mapped into it (alloc_spread); each entry: handle, byte offset, bytes
+    struct VmmChunk {
+        hipMemGenericAllocationHandle_t h;
+        size_t off, bytes;
+    };
+    std::vector<VmmChunk> vmm_chunks;
+    size_t vmm_span = 0;
     float* h_stage = nullptr;     // pinned staging for row-pointer downloads (two halves)
     size_t h_stage_floats = 0;
     size_t stage_half_floats = kStageFloats / 2; // GDP_TUNE_STAGE_KB
@@ -565,6 +574,88 @@ const char* gdp_status_string(int s) {
 
 const char* gdp_last_error(const gdp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
+// GDP_SPREAD_VMM (layout): reserve the pyramid's address range and back it with
+// separately created physical chunks — one per image (default), or GDP_SPREAD_CHUNK_MB-sized pieces
+// of a dense batch.  With GDP_IMAGE_STRIDE_MB the images sit that far apart and the gaps stay
+// unmapped; GDP_SPREAD_PHYS_MB creates that much physical spacer after each chunk and releases the
+// spacers once everything is mapped.  Nothing but placement changes: same offsets, same bits.
+static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
+    Geom& g = c->geom;
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = c->device;
+    size_t gran = 0;
+    hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (e != hipSuccess) {
+        where = "hipMemGetAllocationGranularity";
+        return e;
+    }
+    gran = std::max<size_t>(gran, 256);
+    auto up = [gran](size_t v) { return (v + gran - 1) / gran * gran; };
+    const size_t img = up((size_t)c->img_floats * 4);
+    const size_t stride = up(std::max((size_t)g.pyr_stride * 4, img));
+    g.pyr_stride = (long long)(stride / 4);
+    const size_t span = stride * (size_t)g.batch;
+    const char* ph = std::getenv("GDP_SPREAD_PHYS_MB");
+    const size_t spacer = ph ? up((size_t)std::max(0ll, std::atoll(ph)) << 20) : 0;
+    const char* ck = std::getenv("GDP_SPREAD_CHUNK_MB");
+    const size_t fixed = ck ? up((size_t)std::max(1ll, std::atoll(ck)) << 20) : 0;
+    // the pieces to map: [off, off + bytes)
+    std::vector<std::pair<size_t, size_t>> pieces;
+    if (fixed && stride == img) {
+        for (size_t off = 0; off < span; off += fixed) pieces.push_back({off, std::min(fixed, span - off)});
+    } else {
+        for (int b = 0; b < g.batch; ++b) pieces.push_back({(size_t)b * stride, img});
+    }
+    const bool contiguous = stride == img;  // the pieces tile [0, span) with no unmapped gap
+    void* base = nullptr;
+    where = "granularity " + std::to_string(gran) + ", span " + std::to_string(span) + ", pieces " +
+            std::to_string(pieces.size()) + ": ";
+    if ((e = hipMemAddressReserve(&base, span, gran, nullptr, 0)) != hipSuccess) {
+        where += "hipMemAddressReserve";
+        return e;
+    }
+    c->d_out_own = static_cast<float*>(base);
+    c->vmm_span = span;
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    std::vector<hipMemGenericAllocationHandle_t> spacers;
+    for (size_t i = 0; i < pieces.size() && e == hipSuccess; ++i) {
+        hipMemGenericAllocationHandle_t h;
+        if ((e = hipMemCreate(&h, pieces[i].second, &prop, 0)) != hipSuccess) {
+            where += "hipMemCreate(piece " + std::to_string(i) + ", " + std::to_string(pieces[i].second) + " B)";
+            break;
+        }
+        char* at = static_cast<char*>(base) + pieces[i].first;
+        if ((e = hipMemMap(at, pieces[i].second, 0, h, 0)) != hipSuccess) {
+            where += "hipMemMap(piece " + std::to_string(i) + " at " + std::to_string(pieces[i].first) + ")";
+            (void)hipMemRelease(h);
+            break;
+        }
+        c->vmm_chunks.push_back({h, pieces[i].first, pieces[i].second});  // gdp_destroy unmaps it
+        // access: per piece where gaps stay unmapped, else once over the whole range below (a piece
+        // that is not a multiple of 2 MiB was refused on its own: hipMemSetAccess, r04x)
+        if (!contiguous && (e = hipMemSetAccess(at, pieces[i].second, &acc, 1)) != hipSuccess) {
+            where += "hipMemSetAccess(piece " + std::to_string(i) + ")";
+            break;
+        }
+        if (spacer && i + 1 < pieces.size()) {
+            hipMemGenericAllocationHandle_t sp;
+            if ((e = hipMemCreate(&sp, spacer, &prop, 0)) != hipSuccess) {
+                where += "hipMemCreate(spacer)";
+                break;
+            }
+            spacers.push_back(sp);
+        }
+    }
+    for (hipMemGenericAllocationHandle_t sp : spacers) (void)hipMemRelease(sp);
+    if (e == hipSuccess && contiguous && (e = hipMemSetAccess(base, span, &acc, 1)) != hipSuccess)
+        where += "hipMemSetAccess(whole range)";
+    return e;
+}
+
 int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int row_begin, int row_end, int device) try {
     if (!out) return GDP_ERR_ARG;
     *out = nullptr;
@@ -693,6 +784,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
     g.pyr_stride = round_up(lev_off, kLevelAlign);
+    c->img_floats = g.pyr_stride;
     // optional image stride (MiB) — layout experiment knob, like GDP_LEVEL_PAD: images that far
     // apart, so tile order 1's eight XCD ranges (batch / 8 images each) start 8 x stride apart
     if (const char* is_env = std::getenv("GDP_IMAGE_STRIDE_MB"))
@@ -752,7 +844,11 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     c->d_taps_mode[c->centre_mode] = c->d_taps;
     if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)  // int32
         return hip_fail(e, "hipMalloc(input)");
-    if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
+    if (const char* vm = std::getenv("GDP_SPREAD_VMM"); vm && std::atoi(vm) != 0) {
+        std::string where;
+        if ((e = alloc_spread(c, where)) != hipSuccess)
+            return hip_fail(e, ("spread pyramid (GDP_SPREAD_VMM, " + where + ")").c_str());
+    } else if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(pyramid)");
     c->d_out = c->d_out_own;
     if ((e = hipMalloc(&c->d_sum, sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(sum)");
@@ -787,7 +883,15 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_in_own) (void)hipFree(c->d_in_own);
     for (void* h : c->d_halo_own)
         if (h) (void)hipFree(h);
-    if (c->d_out_own) (void)hipFree(c->d_out_own);
+    if (c->vmm_span) {
+        for (const gdp_ctx::VmmChunk& k : c->vmm_chunks) {
+            (void)hipMemUnmap(reinterpret_cast<char*>(c->d_out_own) + k.off, k.bytes);
+            (void)hipMemRelease(k.h);
+        }
+        if (c->d_out_own) (void)hipMemAddressFree(c->d_out_own, c->vmm_span);
+    } else if (c->d_out_own) {
+        (void)hipFree(c->d_out_own);
+    }
     if (c->d_ctaps) (void)hipFree(c->d_ctaps);
     if (c->d_cradius) (void)hipFree(c->d_cradius);
     if (c->d_conv_perm) (void)hipFree(c->d_conv_perm);
@@ -1491,7 +1595,7 @@ int gdp_upload_image_raw(gdp_ctx* c, int b, const float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_raw: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
-    GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, host, (size_t)c->geom.pyr_stride * 4,
+    GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, host, (size_t)c->img_floats * 4,
                               hipMemcpyHostToDevice, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1550,13 +1654,13 @@ void gdp_host_free(void* host) {
     if (host) (void)hipHostFree(host);
 }
 
-size_t gdp_image_floats(const gdp_ctx* c) { return c ? (size_t)c->geom.pyr_stride : 0; }
+size_t gdp_image_floats(const gdp_ctx* c) { return c ? (size_t)c->img_floats : 0; }
 
 int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_image_raw: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
-    GDP_HIP(c, hipMemcpyAsync(host, c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->geom.pyr_stride * 4,
+    GDP_HIP(c, hipMemcpyAsync(host, c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->img_floats * 4,
                               hipMemcpyDeviceToHost, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;

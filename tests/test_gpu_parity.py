@@ -181,9 +181,17 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
                         _assert_same(ctx.level(b, o, s), lv, ("band", variant, H, W, r0, r1, b, o, s))
 
 
-def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch):
-    """GDP_IMAGE_STRIDE_MB (the XCD-range placement experiment) only moves images
-    apart: every image, level and checksum equals the dense layout's, in both tile orders."""
+@pytest.mark.parametrize("env", [{"GDP_IMAGE_STRIDE_MB": "3"},
+                                 {"GDP_SPREAD_VMM": "1"},
+                                 {"GDP_SPREAD_VMM": "1", "GDP_IMAGE_STRIDE_MB": "5"},
+                                 {"GDP_SPREAD_VMM": "1", "GDP_SPREAD_PHYS_MB": "4"},
+                                 {"GDP_SPREAD_VMM": "1", "GDP_SPREAD_CHUNK_MB": "2"}])
+def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch, env):
+    """The spread layouts (the XCD-range placement experiment, DESIGN §5.1: GDP_IMAGE_STRIDE_MB,
+    and the reserved-range form GDP_SPREAD_VMM with GDP_SPREAD_PHYS_MB physical spacers) only move
+    images apart: every image, level, checksum and raw device-layout copy equals the dense
+    layout's, in both tile orders."""
+    import ctypes
     H, W, B = 300, 500, 3
     imgs = [oracle.lcg_image(H, W, 40 + b) for b in range(B)]
     with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as dense:
@@ -191,16 +199,28 @@ def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch):
             dense.set_input(im, b)
         dense.build()
         sums = [dense.checksum(b) for b in range(B)]
-    monkeypatch.setenv("GDP_IMAGE_STRIDE_MB", "3")
+        n = pkg.lib().gdp_image_floats(dense._ctx)
+        raw = np.empty((B, n), np.float32)
+        for b in range(B):
+            assert pkg.lib().gdp_download_image_raw(dense._ctx, b, raw[b].ctypes.data_as(ctypes.c_void_p)) == 0
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as ctx:
+        assert pkg.lib().gdp_image_floats(ctx._ctx) == n
         for b, im in enumerate(imgs):
             ctx.set_input(im, b)
         for order in (0, 1):
             ctx.set_tuning(variant=0, tile_order=order)
             ctx.build()
             for b, im in enumerate(imgs):
-                _assert_same(ctx.pyramid(b), oracle.build_pyramid(im, 2, 5), ("stride", order, b))
+                _assert_same(ctx.pyramid(b), oracle.build_pyramid(im, 2, 5), ("stride", env, order, b))
                 assert ctx.checksum(b) == sums[b]
+        got = np.empty(n, np.float32)
+        for b in range(B):  # raw copies cover the dense extent only (the gaps may be unmapped)
+            assert pkg.lib().gdp_download_image_raw(ctx._ctx, b, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            assert np.array_equal(got.view(np.uint32), raw[b].view(np.uint32))
+        assert pkg.lib().gdp_upload_image_raw(ctx._ctx, 1, raw[0].ctypes.data_as(ctypes.c_void_p)) == 0
+        assert ctx.checksum(1) == sums[0]
 
 
 def test_default_variant_follows_geometry(pkg):

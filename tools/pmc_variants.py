@@ -44,12 +44,14 @@ def run(args):
             c.set_window_centre("intlen")
         c.sync()
     order = []
+    only = {int(x) for x in args.variants.split(",")} if args.variants else None
     for v in range(64):
         try:
             ctxs[0].set_tuning(variant=v)
         except pkg.GdpError:
             break
-        order += [(v, 0), (v, 1)]
+        if only is None or v in only:
+            order += [(v, 0), (v, 1)]
     manifest = []
     for v, t in order:
         for c in ctxs:
@@ -65,7 +67,9 @@ def run(args):
         c.close()
     with open(args.manifest, "w") as f:
         json.dump({"config": args.config, "op": args.op, "rotate": rotate, "zero_window": args.zero_window,
-                   "band_of": args.band_of, "band": [r0, r1], "instances": manifest}, f)
+                   "band_of": args.band_of, "band": [r0, r1], "instances": manifest,
+                   "image_stride_mb": int(os.environ["GDP_IMAGE_STRIDE_MB"]) if os.environ.get("GDP_IMAGE_STRIDE_MB")
+                   else None}, f)
 
 
 def band_rows(pkg, cfg, band_of):
@@ -121,6 +125,7 @@ def summarise(args):
                "tile_order": m["tile_order"], "input_format": "i32", "op": man.get("op", "build"),
                "zero_window": man.get("zero_window", 0),
                **({"band_of": band_of, "band_rows": [r0, r1]} if band_of else {}),
+               **({"image_stride_mb": man["image_stride_mb"]} if man.get("image_stride_mb") else {}),
                "source": "tools/pmc_variants.py: every instance in one process, its own FETCH_SIZE and WRITE_SIZE "
                          "rocprofv3 --pmc passes, launches cycling over %d cold buffer sets as in bench.py" % man["rotate"],
                "dispatches_counted": [len(fs), len(ws)],
@@ -130,7 +135,7 @@ def summarise(args):
                "traffic_over_algorithmic": (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads); write = WRITE_SIZE KiB"}
         tag = man["config"] + (f"b{band_of}" if band_of else "") + ("_subset" if man.get("op") == "subset" else "")
-        zw = "z1" if man.get("zero_window", 0) else ""
+        zw = ("z1" if man.get("zero_window", 0) else "") + (f"s{man['image_stride_mb']}" if man.get("image_stride_mb") else "")
         out = os.path.join(REPO, "profiles", f"pmc_{tag}_v{m['variant']}o{m['tile_order']}{zw}_{args.round}.json")
         if os.path.exists(out) and not args.overwrite:
             print("keep", out)
@@ -151,6 +156,7 @@ def main():
                     help="subset: the GenerateDoG_nomp_dynamic build (bench.py --op subset)")
     ap.add_argument("--zero-window", type=int, default=0, choices=[0, 1],
                     help="GDP_TUNE_ZERO_WINDOW of every instance (records pmc_<cfg>_v<V>o<T>z1_*.json)")
+    ap.add_argument("--variants", default=None, help="comma-separated variant numbers to profile (default: all)")
     ap.add_argument("--band-of", type=int, default=None,
                     help="row-band config: profile rank 0's band of N ranks (bench.py --gpus N --config c5's "
                          "per-rank launch; records pmc_c5b<N>_*.json)")
