@@ -227,16 +227,18 @@ def latest_conv_pmc(config_key, tun):
 
 
 def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0, band_of=None,
-               image_stride_mb=None):
+               image_stride_mb=None, chunk_kb=None):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
     profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
     whose recorded build variant, tile order and zero-window mode equal the run's; None when no profile of that
     instance exists (the traffic of another variant would describe a different kernel).  band_of = N:
     the row-band config's per-rank launch at N ranks (rank 0's band of N, profiled on one GPU by
     tools/pmc_variants.py --band-of N), not the whole image's.  image_stride_mb: the spread layout's
-    records (GDP_IMAGE_STRIDE_MB), kept apart from the dense layout's."""
+    records (GDP_IMAGE_STRIDE_MB), kept apart from the dense layout's.  chunk_kb: the run's pyramid
+    backing (GDP_TUNE_PYRAMID_CHUNK_KB); a record of the same backing is preferred, else one of
+    another backing (the backing moves pages, not bytes: DESIGN.md §4) — the file is named either way."""
     pdir = os.path.join(REPO, "profiles")
-    best = None
+    best, same = None, None
     if os.path.isdir(pdir):
         for f in sorted(os.listdir(pdir)):
             if f.startswith("pmc_") and f.endswith(".json"):
@@ -254,7 +256,9 @@ def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_windo
                         rec.get("image_stride_mb") == image_stride_mb and \
                         lt in rec.get("kernel", lt):
                     best = dict(rec, file=f)
-    return best
+                    if rec.get("pyramid_chunk_kb", 0) == (chunk_kb or 0):
+                        same = best
+    return same or best
 
 
 def latest_inplace_pmc(config_key, op, tun):
@@ -1034,7 +1038,7 @@ def main():
     pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3,
                       tun["zero_window"] if args.op == "build" else 0, band_of=band_of,
                       image_stride_mb=int(os.environ["GDP_IMAGE_STRIDE_MB"]) if os.environ.get("GDP_IMAGE_STRIDE_MB")
-                      else None)
+                      else None, chunk_kb=tun.get("pyramid_chunk_kb", 0))
            if args.op in ("build", "subset") and args.input == "i32" and (band_of is None or rank == 0) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
@@ -1062,6 +1066,9 @@ def main():
             "input_format": "int32" if args.input == "i32" else "uint8",
             "rotated_buffer_sets": rotate,
             "working_set_bytes_per_gpu": rotate * set_bytes,
+            "pyramid_backing": ("one hipMalloc" if ctx.tuning()["pyramid_chunk_kb"] == 0 else
+                                "one physical piece per image (VMM)" if ctx.tuning()["pyramid_chunk_kb"] < 0 else
+                                "%d KiB physical pieces mapped into one range (VMM)" % ctx.tuning()["pyramid_chunk_kb"]),
             **({"layout": {"GDP_IMAGE_STRIDE_MB": int(os.environ["GDP_IMAGE_STRIDE_MB"]),
                            "note": "images spread out (DESIGN.md §5.1 XCD-range placement): same bytes moved, "
                                    "larger allocation",

@@ -333,9 +333,12 @@ enum {
                                    most n memory operations of the wave are outstanding
                                    (s_waitcnt vmcnt(n)); the same bits either way */
     GDP_TUNE_CONV_PACE = 18,    /* the same for gdp_build_gaussian's block tiles (default 2) */
-    GDP_TUNE_INPLACE_PACE = 19  /* the same for the in-place re-entry (gdp_generate_dog, k_levels;
+    GDP_TUNE_INPLACE_PACE = 19, /* the same for the in-place re-entry (gdp_generate_dog, k_levels;
                                    default -1): its own field, so tuning the build's pacing never
                                    changes the in-place passes' speed */
+    GDP_TUNE_PYRAMID_CHUNK_KB = 20 /* read-only: how the context-owned pyramid is backed — KiB per
+                                      separately created physical piece (default 2 MiB, at most
+                                      4096 pieces), -1 one piece per image, 0 one hipMalloc */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* Benchmark every build-kernel variant x tile order x store mode (GDP_TUNE_ZERO_WINDOW,

@@ -29,6 +29,7 @@ GDP_TUNE_ZERO_WINDOW = 16
 GDP_TUNE_STORE_PACE = 17
 GDP_TUNE_CONV_PACE = 18
 GDP_TUNE_INPLACE_PACE = 19
+GDP_TUNE_PYRAMID_CHUNK_KB = 20
 
 
 class GdpError(RuntimeError):

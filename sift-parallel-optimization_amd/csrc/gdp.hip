@@ -122,6 +122,7 @@ struct gdp_ctx {
     };
     std::vector<VmmChunk> vmm_chunks;
     size_t vmm_span = 0;
+    int pyr_chunk_kb = 0;         // GDP_TUNE_PYRAMID_CHUNK_KB: 0 one hipMalloc, -1 one chunk per image
     float* h_stage = nullptr;     // pinned staging for row-pointer downloads (two halves)
     size_t h_stage_floats = 0;
     size_t stage_half_floats = kStageFloats / 2; // GDP_TUNE_STAGE_KB
@@ -574,6 +575,23 @@ const char* gdp_status_string(int s) {
 
 const char* gdp_last_error(const gdp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
+// Release the context-owned pyramid (one hipMalloc, or alloc_spread's chunks and range).
+static void free_pyramid(gdp_ctx* c) {
+    if (c->vmm_span) {
+        for (const gdp_ctx::VmmChunk& k : c->vmm_chunks) {
+            (void)hipMemUnmap(reinterpret_cast<char*>(c->d_out_own) + k.off, k.bytes);
+            (void)hipMemRelease(k.h);
+        }
+        if (c->d_out_own) (void)hipMemAddressFree(c->d_out_own, c->vmm_span);
+    } else if (c->d_out_own) {
+        (void)hipFree(c->d_out_own);
+    }
+    c->vmm_chunks.clear();
+    c->vmm_span = 0;
+    c->d_out_own = nullptr;
+    c->pyr_chunk_kb = 0;
+}
+
 // GDP_SPREAD_VMM (layout): reserve the pyramid's address range and back it with
 // separately created physical chunks — one per image (default), or GDP_SPREAD_CHUNK_MB-sized pieces
 // of a dense batch.  With GDP_IMAGE_STRIDE_MB the images sit that far apart and the gaps stay
@@ -599,14 +617,23 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     const size_t span = stride * (size_t)g.batch;
     const char* ph = std::getenv("GDP_SPREAD_PHYS_MB");
     const size_t spacer = ph ? up((size_t)std::max(0ll, std::atoll(ph)) << 20) : 0;
+    // default piece: 2 MiB (at most 4096 pieces: larger pyramids take larger pieces).  Measured
+    // against one hipMalloc (tools/tune.py A/B, profiles/chunk_*_r04z.log, vmm_*_r04y.log): 4096^2
+    // 0.0789 vs 0.0860 ms, 64 x 1080x1920 0.606 vs 0.684, 16384^2 1.175 vs 1.218-1.261 on one box
+    // and equal on another, 64 x 4096^2 within 1 %; 512 MiB+ pieces behave like one allocation.
+    // GDP_SPREAD_CHUNK_MB = n MiB pieces, 0 = one piece per image.
     const char* ck = std::getenv("GDP_SPREAD_CHUNK_MB");
-    const size_t fixed = ck ? up((size_t)std::max(1ll, std::atoll(ck)) << 20) : 0;
+    const size_t two = (size_t)2 << 20;
+    const size_t fixed = ck ? (std::atoll(ck) > 0 ? up((size_t)std::atoll(ck) << 20) : 0)
+                            : up(std::max(two, (span / 4096 + two - 1) / two * two));
     // the pieces to map: [off, off + bytes)
     std::vector<std::pair<size_t, size_t>> pieces;
     if (fixed && stride == img) {
         for (size_t off = 0; off < span; off += fixed) pieces.push_back({off, std::min(fixed, span - off)});
+        c->pyr_chunk_kb = (int)(fixed >> 10);
     } else {
         for (int b = 0; b < g.batch; ++b) pieces.push_back({(size_t)b * stride, img});
+        c->pyr_chunk_kb = -1;
     }
     const bool contiguous = stride == img;  // the pieces tile [0, span) with no unmapped gap
     void* base = nullptr;
@@ -844,11 +871,22 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     c->d_taps_mode[c->centre_mode] = c->d_taps;
     if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)  // int32
         return hip_fail(e, "hipMalloc(input)");
-    if (const char* vm = std::getenv("GDP_SPREAD_VMM"); vm && std::atoi(vm) != 0) {
+    // The pyramid: separately created physical pieces mapped into one address range (alloc_spread;
+    // default), or one hipMalloc (GDP_SPREAD_VMM=0, or when the VMM calls are refused).
+    bool pyr_done = false;
+    const char* vm = std::getenv("GDP_SPREAD_VMM");
+    if (!vm || std::atoi(vm) != 0) {
         std::string where;
-        if ((e = alloc_spread(c, where)) != hipSuccess)
+        if ((e = alloc_spread(c, where)) == hipSuccess) {
+            pyr_done = true;
+        } else if (vm) {
             return hip_fail(e, ("spread pyramid (GDP_SPREAD_VMM, " + where + ")").c_str());
-    } else if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
+        } else {
+            free_pyramid(c);  // not asked for explicitly: one hipMalloc instead
+            (void)hipGetLastError();
+        }
+    }
+    if (!pyr_done && (e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(pyramid)");
     c->d_out = c->d_out_own;
     if ((e = hipMalloc(&c->d_sum, sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(sum)");
@@ -883,15 +921,7 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_in_own) (void)hipFree(c->d_in_own);
     for (void* h : c->d_halo_own)
         if (h) (void)hipFree(h);
-    if (c->vmm_span) {
-        for (const gdp_ctx::VmmChunk& k : c->vmm_chunks) {
-            (void)hipMemUnmap(reinterpret_cast<char*>(c->d_out_own) + k.off, k.bytes);
-            (void)hipMemRelease(k.h);
-        }
-        if (c->d_out_own) (void)hipMemAddressFree(c->d_out_own, c->vmm_span);
-    } else if (c->d_out_own) {
-        (void)hipFree(c->d_out_own);
-    }
+    free_pyramid(c);
     if (c->d_ctaps) (void)hipFree(c->d_ctaps);
     if (c->d_cradius) (void)hipFree(c->d_cradius);
     if (c->d_conv_perm) (void)hipFree(c->d_conv_perm);
@@ -1808,6 +1838,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
+        case GDP_TUNE_PYRAMID_CHUNK_KB: *value = c->pyr_chunk_kb; return GDP_OK;
         default: return GDP_ERR_ARG;
     }
 } GDP_ABI_CATCH(c)

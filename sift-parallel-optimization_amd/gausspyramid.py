@@ -257,7 +257,7 @@ class PyramidContext:
 
     _TUNING = ("nontemporal", "blocks_per_cu", "grid", "variant", "tile_order", "inplace_sub", "window_sub",
                "conv_kernel", "conv_rows", "conv_order", "build_lds", "stage_kb", "stage_threads", "conv_waves", "zero_window",
-               "store_pace", "conv_pace", "inplace_pace")
+               "store_pace", "conv_pace", "inplace_pace", "pyramid_chunk_kb")  # the last one read-only
 
     @staticmethod
     def _tuning_key(name):

@@ -223,6 +223,24 @@ def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch, env):
         assert ctx.checksum(1) == sums[0]
 
 
+def test_pyramid_backing_default_and_opt_out(pkg, oracle, monkeypatch):
+    """Default: the pyramid lives in separately created 2 MiB physical pieces (at most 4096 of
+    them); GDP_SPREAD_VMM=0 gives one hipMalloc — identical bits either way."""
+    img = oracle.lcg_image(700, 900, 9)
+    want = oracle.build_pyramid(img, 2, 5)
+    with pkg.PyramidContext(700, 900, S=2, octaves=5) as ctx:
+        assert ctx.tuning()["pyramid_chunk_kb"] == 2048
+        ctx.set_input(img)
+        ctx.build()
+        _assert_same(ctx.pyramid(0), want, "chunked")
+    monkeypatch.setenv("GDP_SPREAD_VMM", "0")
+    with pkg.PyramidContext(700, 900, S=2, octaves=5) as ctx:
+        assert ctx.tuning()["pyramid_chunk_kb"] == 0
+        ctx.set_input(img)
+        ctx.build()
+        _assert_same(ctx.pyramid(0), want, "one allocation")
+
+
 def test_default_variant_follows_geometry(pkg):
     with pkg.PyramidContext(64, 4096, S=2, batch=2) as a, pkg.PyramidContext(64, 1920, S=2) as b, \
             pkg.PyramidContext(4096, 4096, S=2, octaves=5) as c:

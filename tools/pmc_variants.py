@@ -63,13 +63,14 @@ def run(args):
         for c in ctxs:
             c.sync()
         manifest.append({"variant": v, "tile_order": t, "dispatches": n, "warm": args.warm})
+    chunk_kb = ctxs[0].tuning().get("pyramid_chunk_kb", 0)
     for c in ctxs:
         c.close()
     with open(args.manifest, "w") as f:
         json.dump({"config": args.config, "op": args.op, "rotate": rotate, "zero_window": args.zero_window,
                    "band_of": args.band_of, "band": [r0, r1], "instances": manifest,
                    "image_stride_mb": int(os.environ["GDP_IMAGE_STRIDE_MB"]) if os.environ.get("GDP_IMAGE_STRIDE_MB")
-                   else None}, f)
+                   else None, "pyramid_chunk_kb": chunk_kb}, f)
 
 
 def band_rows(pkg, cfg, band_of):
@@ -126,6 +127,7 @@ def summarise(args):
                "zero_window": man.get("zero_window", 0),
                **({"band_of": band_of, "band_rows": [r0, r1]} if band_of else {}),
                **({"image_stride_mb": man["image_stride_mb"]} if man.get("image_stride_mb") else {}),
+               **({"pyramid_chunk_kb": man["pyramid_chunk_kb"]} if man.get("pyramid_chunk_kb") else {}),
                "source": "tools/pmc_variants.py: every instance in one process, its own FETCH_SIZE and WRITE_SIZE "
                          "rocprofv3 --pmc passes, launches cycling over %d cold buffer sets as in bench.py" % man["rotate"],
                "dispatches_counted": [len(fs), len(ws)],
@@ -135,7 +137,8 @@ def summarise(args):
                "traffic_over_algorithmic": (read_b + write_b) / alg,
                "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads); write = WRITE_SIZE KiB"}
         tag = man["config"] + (f"b{band_of}" if band_of else "") + ("_subset" if man.get("op") == "subset" else "")
-        zw = ("z1" if man.get("zero_window", 0) else "") + (f"s{man['image_stride_mb']}" if man.get("image_stride_mb") else "")
+        zw = ("z1" if man.get("zero_window", 0) else "") + (f"s{man['image_stride_mb']}" if man.get("image_stride_mb") else "") \
+            + (f"k{man['pyramid_chunk_kb']}" if man.get("pyramid_chunk_kb") else "")
         out = os.path.join(REPO, "profiles", f"pmc_{tag}_v{m['variant']}o{m['tile_order']}{zw}_{args.round}.json")
         if os.path.exists(out) and not args.overwrite:
             print("keep", out)
