@@ -283,9 +283,9 @@ class PyramidContext:
                     conv_rows=conv_rows, conv_order=conv_order, build_lds=build_lds, stage_kb=stage_kb,
                     stage_threads=stage_threads, conv_waves=conv_waves, zero_window=zero_window,
                     store_pace=store_pace, conv_pace=conv_pace, inplace_pace=inplace_pace)
-        for name in self._TUNING:
-            if vals[name] is not None:
-                check(lib().gdp_set_tuning(self._ctx, self._tuning_key(name), int(vals[name])), self._ctx)
+        for name, val in vals.items():
+            if val is not None:
+                check(lib().gdp_set_tuning(self._ctx, self._tuning_key(name), int(val)), self._ctx)
 
     def autotune(self, iters=5, stream=None):
         """Time every build variant x tile order x store mode (zero_window, store_pace) on the
