@@ -89,6 +89,11 @@ struct gdp_ctx {
     Geom geom{};
     Geom* d_geom = nullptr;
     void* d_in_own = nullptr;     // context-owned input buffer (int32 or uint8 per geom.in_fmt)
+    // GDP_INPUT_VMM=1 (experiment): the input in 2 MiB physical pieces like the pyramid (in_vmm_*)
+    struct VmmBuf {
+        std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;  // handle, offset
+        size_t span = 0;  // 0: the buffer is one hipMalloc
+    } in_vmm;
     void* d_halo_own[2] = {nullptr, nullptr}; // context-owned halo rows above / below a band (conv extension)
     const void* d_in = nullptr;   // buffer the kernels read (own or caller's)
     float* d_out = nullptr;
@@ -575,6 +580,52 @@ const char* gdp_status_string(int s) {
 
 const char* gdp_last_error(const gdp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
+// The input buffer: one hipMalloc, or (GDP_INPUT_VMM=1) 2 MiB physical pieces in one 2 MiB-aligned
+// range; `vb` records which (free_input releases either form).
+static hipError_t alloc_input(gdp_ctx* c, size_t bytes, void** out, gdp_ctx::VmmBuf& vb) {
+    bytes = std::max<size_t>(16, bytes);
+    *out = nullptr;
+    const char* iv = std::getenv("GDP_INPUT_VMM");
+    if (!iv || std::atoi(iv) == 0) return hipMalloc(out, bytes);
+    const size_t two = (size_t)2 << 20, span = (bytes + two - 1) / two * two;
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = c->device;
+    void* base = nullptr;
+    hipError_t e = hipMemAddressReserve(&base, span, two, nullptr, 0);
+    if (e != hipSuccess) return e;
+    vb.span = span;
+    *out = base;
+    for (size_t off = 0; off < span && e == hipSuccess; off += two) {
+        hipMemGenericAllocationHandle_t h;
+        if ((e = hipMemCreate(&h, two, &prop, 0)) != hipSuccess) break;
+        if ((e = hipMemMap(static_cast<char*>(base) + off, two, 0, h, 0)) != hipSuccess) {
+            (void)hipMemRelease(h);
+            break;
+        }
+        vb.chunks.push_back({h, off});
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    if (e == hipSuccess) e = hipMemSetAccess(base, span, &acc, 1);
+    return e;
+}
+
+static void free_input(void* p, gdp_ctx::VmmBuf& vb) {
+    if (vb.span && p) {
+        for (const auto& k : vb.chunks) {
+            (void)hipMemUnmap(static_cast<char*>(p) + k.second, (size_t)2 << 20);
+            (void)hipMemRelease(k.first);
+        }
+        (void)hipMemAddressFree(p, vb.span);
+    } else if (p) {
+        (void)hipFree(p);
+    }
+    vb = gdp_ctx::VmmBuf{};
+}
+
 // Release the context-owned pyramid (one hipMalloc, or alloc_spread's chunks and range).
 static void free_pyramid(gdp_ctx* c) {
     if (c->vmm_span) {
@@ -622,10 +673,13 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     // 0.0789 vs 0.0860 ms, 64 x 1080x1920 0.606 vs 0.684, 16384^2 1.175 vs 1.218-1.261 on one box
     // and equal on another, 64 x 4096^2 within 1 %; 512 MiB+ pieces behave like one allocation.
     // GDP_SPREAD_CHUNK_MB = n MiB pieces, 0 = one piece per image.
+    // (GDP_SPREAD_CHUNK_KB: the same in KiB — below 2 MiB only for measurement: 37-62 % of 8 TB/s)
     const char* ck = std::getenv("GDP_SPREAD_CHUNK_MB");
+    const char* ckk = std::getenv("GDP_SPREAD_CHUNK_KB");
     const size_t two = (size_t)2 << 20;
-    const size_t fixed = ck ? (std::atoll(ck) > 0 ? up((size_t)std::atoll(ck) << 20) : 0)
-                            : up(std::max(two, (span / 4096 + two - 1) / two * two));
+    const size_t fixed = ckk ? (std::atoll(ckk) > 0 ? up((size_t)std::atoll(ckk) << 10) : 0)
+                       : ck  ? (std::atoll(ck) > 0 ? up((size_t)std::atoll(ck) << 20) : 0)
+                             : up(std::max(two, (span / 4096 + two - 1) / two * two));
     // the pieces to map: [off, off + bytes)
     std::vector<std::pair<size_t, size_t>> pieces;
     if (fixed && stride == img) {
@@ -639,7 +693,9 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     void* base = nullptr;
     where = "granularity " + std::to_string(gran) + ", span " + std::to_string(span) + ", pieces " +
             std::to_string(pieces.size()) + ": ";
-    if ((e = hipMemAddressReserve(&base, span, gran, nullptr, 0)) != hipSuccess) {
+    // 2 MiB-aligned range: a 2 MiB piece then covers exactly one large page (pieces below 2 MiB
+    // ran 2-2.5x slower, 256 KiB-1 MiB: profiles/kb_*_r04ad.log)
+    if ((e = hipMemAddressReserve(&base, span, std::max(gran, two), nullptr, 0)) != hipSuccess) {
         where += "hipMemAddressReserve";
         return e;
     }
@@ -869,7 +925,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     if ((e = hipMalloc(&c->d_taps, std::max<size_t>(4, c->h_taps.size() * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(taps)");
     c->d_taps_mode[c->centre_mode] = c->d_taps;
-    if ((e = hipMalloc(&c->d_in_own, std::max<size_t>(16, (size_t)g.in_img_stride * batch * 4))) != hipSuccess)  // int32
+    if ((e = alloc_input(c, (size_t)g.in_img_stride * batch * 4, &c->d_in_own, c->in_vmm)) != hipSuccess)  // int32
         return hip_fail(e, "hipMalloc(input)");
     // The pyramid: separately created physical pieces mapped into one address range (alloc_spread;
     // default), or one hipMalloc (GDP_SPREAD_VMM=0, or when the VMM calls are refused).
@@ -918,7 +974,7 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->d_geom) (void)hipFree(c->d_geom);
     for (float* t : c->d_taps_mode)
         if (t) (void)hipFree(t);
-    if (c->d_in_own) (void)hipFree(c->d_in_own);
+    free_input(c->d_in_own, c->in_vmm);
     for (void* h : c->d_halo_own)
         if (h) (void)hipFree(h);
     free_pyramid(c);
@@ -1058,14 +1114,17 @@ int gdp_set_input_format(gdp_ctx* c, int fmt) try {
     GDP_HIP(c, hipDeviceSynchronize());
     const size_t bytes = (size_t)c->in_img_stride_own * c->geom.batch * (fmt == GDP_INPUT_U8 ? 1 : 4);
     void* fresh = nullptr;
-    hipError_t e = hipMalloc(&fresh, std::max<size_t>(16, bytes));
-    if (e != hipSuccess) return c->status(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, "hipMalloc(input)");
-    if ((e = hipMemset(fresh, 0, std::max<size_t>(16, bytes))) != hipSuccess) {
-        (void)hipFree(fresh);
-        return c->status(GDP_ERR_HIP, "hipMemset(input): %s", hipGetErrorString(e));
+    gdp_ctx::VmmBuf vb;
+    hipError_t e = alloc_input(c, bytes, &fresh, vb);
+    if (e == hipSuccess) e = hipMemset(fresh, 0, std::max<size_t>(16, bytes));
+    if (e != hipSuccess) {  // the context keeps its current input buffer
+        free_input(fresh, vb);
+        return c->status(e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP, "allocating the input: %s",
+                         hipGetErrorString(e));
     }
-    GDP_HIP(c, hipFree(c->d_in_own));
+    free_input(c->d_in_own, c->in_vmm);
     c->d_in_own = fresh;
+    c->in_vmm = std::move(vb);
     c->geom.in_fmt = fmt;
     for (int side = 0; side < 2; ++side) { // halo rows follow the input format: re-created on next use
         if (c->d_halo_own[side]) GDP_HIP(c, hipFree(c->d_halo_own[side]));
