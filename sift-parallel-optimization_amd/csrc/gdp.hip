@@ -705,7 +705,22 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     acc.location = prop.location;
     acc.flags = hipMemAccessFlagsProtReadWrite;
     std::vector<hipMemGenericAllocationHandle_t> spacers;
-    for (size_t i = 0; i < pieces.size() && e == hipSuccess; ++i) {
+    // GDP_SPREAD_PERM (experiment): the order the physical pieces are created in — 0 in address
+    // order, 1 residue classes mod 8 (pieces 0, 8, 16, .., then 1, 9, ..), 2 last piece first
+    const char* pm = std::getenv("GDP_SPREAD_PERM");
+    const int perm = pm ? std::atoi(pm) : 0;
+    const size_t np = pieces.size();
+    auto piece_at = [&](size_t k) -> size_t {
+        if (perm == 1) {
+            auto count = [np](size_t r) { return r < np ? (np - r + 7) / 8 : 0; };  // pieces r, r + 8, ...
+            size_t r = 0, kk = k;
+            while (r < 7 && kk >= count(r)) kk -= count(r++);
+            return r + 8 * kk;
+        }
+        return perm == 2 ? np - 1 - k : k;
+    };
+    for (size_t k = 0; k < np && e == hipSuccess; ++k) {
+        const size_t i = piece_at(k);
         hipMemGenericAllocationHandle_t h;
         if ((e = hipMemCreate(&h, pieces[i].second, &prop, 0)) != hipSuccess) {
             where += "hipMemCreate(piece " + std::to_string(i) + ", " + std::to_string(pieces[i].second) + " B)";
@@ -724,7 +739,7 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
             where += "hipMemSetAccess(piece " + std::to_string(i) + ")";
             break;
         }
-        if (spacer && i + 1 < pieces.size()) {
+        if (spacer && k + 1 < np) {
             hipMemGenericAllocationHandle_t sp;
             if ((e = hipMemCreate(&sp, spacer, &prop, 0)) != hipSuccess) {
                 where += "hipMemCreate(spacer)";
