@@ -186,7 +186,8 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
                                  {"GDP_SPREAD_VMM": "1", "GDP_IMAGE_STRIDE_MB": "5"},
                                  {"GDP_SPREAD_VMM": "1", "GDP_SPREAD_PHYS_MB": "4"},
                                  {"GDP_SPREAD_VMM": "1", "GDP_SPREAD_CHUNK_MB": "2"},
-                                 {"GDP_INPUT_VMM": "1"}, {"GDP_SPREAD_PERM": "1"}, {"GDP_SPREAD_PERM": "2"}])
+                                 {"GDP_INPUT_VMM": "1"}, {"GDP_SPREAD_PERM": "1"}, {"GDP_SPREAD_PERM": "2"},
+                                 {"GDP_SPREAD_PERM": "0"}])
 def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch, env):
     """The spread layouts (the XCD-range placement experiment, DESIGN §5.1: GDP_IMAGE_STRIDE_MB,
     and the reserved-range form GDP_SPREAD_VMM with GDP_SPREAD_PHYS_MB physical spacers) only move
