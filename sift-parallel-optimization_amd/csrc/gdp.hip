@@ -973,6 +973,10 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     }
     if (!pyr_done && (e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
         return hip_fail(e, "hipMalloc(pyramid)");
+    // On the chunked backing v11's tile runs faster in its flattened form v17 (same 8 x 384 tile,
+    // same geometry): 64 x 1080x1920 0.637 vs 0.698 ms with the default store modes
+    // (profiles/defvar_c3_r04am.log); on one hipMalloc v11 stays ahead (0.68-0.69 vs 0.78)
+    if (pyr_done && c->variant == 11) c->variant = 17;
     c->d_out = c->d_out_own;
     if ((e = hipMalloc(&c->d_sum, sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(sum)");
     c->d_in = c->d_in_own;
