@@ -419,11 +419,7 @@ def autotune_rotating(ctxs, stream, iters, rounds=5, op="build"):
 
     pkg = entry.load_package()
     cands = []
-    for v in range(64):
-        try:
-            ctxs[0].set_tuning(variant=v)
-        except pkg.GdpError:
-            break
+    for v in pkg.build_variants():
         # the subset build has no zero window (its levels S..S+2 keep x) but its five stores per group
         # go out with only two windows' loads between them: pacing alone
         modes = ((0, -1), (0, 1), (1, -1), (1, 0)) if op == "build" else ((0, -1), (0, 0), (0, 1))
@@ -928,6 +924,7 @@ def main():
         if args.op == "subset":  # that header's integer-length window centre (the same taps at these sizes)
             c.set_window_centre("intlen")
     autotuned = None
+    t_tune = time.perf_counter()
     if args.variant is not None:
         for c in ctxs:
             c.set_tuning(variant=args.variant, tile_order=args.tile_order, zero_window=args.zero_window,
@@ -971,6 +968,7 @@ def main():
                 c.set_tuning(**{key: args.inplace_sub}, zero_window=args.zero_window, inplace_pace=args.store_pace)
         elif not args.no_autotune:
             autotuned = (key, autotune_inplace(ctxs, steps_fn, stream, 3 if B * H * W > (1 << 28) else 10, key, values))
+    tune_s = time.perf_counter() - t_tune if autotuned else 0.0
     n_step = [0]
 
     def step(st):  # step i works on buffer set i mod rotate
@@ -1037,8 +1035,7 @@ def main():
     band_of = world if (cfg["band"] and world > 1) else None
     pmc = (latest_pmc(args.config, tun["variant"], tun["tile_order"], args.op, S + 3,
                       tun["zero_window"] if args.op == "build" else 0, band_of=band_of,
-                      image_stride_mb=int(os.environ["GDP_IMAGE_STRIDE_MB"]) if os.environ.get("GDP_IMAGE_STRIDE_MB")
-                      else None, chunk_kb=tun.get("pyramid_chunk_kb", 0))
+                      chunk_kb=tun.get("pyramid_chunk_kb", 0))
            if args.op in ("build", "subset") and args.input == "i32" and (band_of is None or rank == 0) else None)
     if args.op == "conv" and args.input == "i32" and not (cfg["band"] and world > 1):
         pmc = latest_conv_pmc(args.config, tun)
@@ -1069,12 +1066,6 @@ def main():
             "pyramid_backing": ("one hipMalloc" if ctx.tuning()["pyramid_chunk_kb"] == 0 else
                                 "one physical piece per image (VMM)" if ctx.tuning()["pyramid_chunk_kb"] < 0 else
                                 "%d KiB physical pieces mapped into one range (VMM)" % ctx.tuning()["pyramid_chunk_kb"]),
-            **({"layout": {"GDP_IMAGE_STRIDE_MB": int(os.environ["GDP_IMAGE_STRIDE_MB"]),
-                           "note": "images spread out (DESIGN.md §5.1 XCD-range placement): same bytes moved, "
-                                   "larger allocation",
-                           "allocated_pyramid_bytes_per_set": (1 if cfg["band"] else B) * max(
-                               4 * (S + 3) * pyramid_pixels(H, W, O), int(os.environ["GDP_IMAGE_STRIDE_MB"]) << 20)}}
-               if os.environ.get("GDP_IMAGE_STRIDE_MB") else {}),
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1126,6 +1117,10 @@ def main():
         {"status": "extension: no reference output (tests/ check it against a float64 convolution)"})
     if result["parity"] is None:  # an in-place op on the row-band config
         result["parity"] = {"status": "unchecked (no reference re-entry fixture of this workload)"}
+    if autotuned:  # outside the timed region: the search that picked the kernel instance
+        result["autotune"] = {"seconds": round(tune_s, 2), "candidates": (
+            len(pkg.build_variants()) * (8 if args.op == "build" else 6) if args.op in ("build", "subset")
+            else None), "rounds": 5}
     result["topology"] = topology
     if distribution is not None:
         result["distribution"] = distribution

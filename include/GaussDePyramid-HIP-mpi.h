@@ -11,41 +11,40 @@
 //
 // Semantics.  The reference's GenerateDoG_mpi needs >= S+4 ranks: ranks i < S+3 filter scale i
 // of every octave and send each row to rank S+3, the collector, which forms all DoG levels
-// (:265-335); the collector's GaussPy ends as the full pyramid.  Here ANY number of ranks works:
-// rank r builds row band gdp_band_rows(n, size, r, layer) of every level on GPU r % devices,
-// and rank 0 — the collector — receives every band into its whole-image context and mirrors it
-// into GaussPy.  Worker state differs from the reference's, by design: there rank i < S+3 ends
-// holding scale i of every octave windowed (the other scales keep their GaussPyInit values, :271-291),
-// rank S+3 is the collector and ranks > S+3 are untouched; here the collector is rank 0 and every
-// other rank's GaussPy keeps what it held before the call (its band's rows live only in its device
-// band context).  No caller in the reference reads a worker's GaussPy (main.cpp:61-74 only times
-// the call), and the reference's role map needs >= S+4 ranks where this one takes any number.
-// The collector's pyramid is bit-identical to the reference's collector for EVERY
-// n: GenerateDoG_mpi centres its windows on the integer octave length (`l = float(len-1)/2`,
+// (:265-335); the collector's GaussPy ends as the full pyramid.  Two role maps are provided:
+//  - ROLES_BANDS (default, `roles`): ANY number of ranks; rank r builds row band
+//    gdp_band_rows(n, size, r, layer) of every level on GPU r % devices, and rank 0 — the
+//    collector (collector() == 0) — receives every band into its whole-image context
+//    (gdp_comm_gather_bands) and mirrors it into GaussPy.  A worker's GaussPy keeps what it held
+//    before the call (its band's rows live only in its device band context), where the
+//    reference's worker i < S+3 ends holding scale i windowed; no caller in the reference reads a
+//    worker's GaussPy (main.cpp:61-74 only times the call).
+//  - ROLES_REFERENCE (opt-in; needs >= S+4 ranks, aborts below): the reference's own roles —
+//    rank i < S+3 windows scale i of every octave of its own state (gdp_gauss_scales, integer-
+//    length centre) and sends it to rank S+3 (gdp_comm_collect_scales), which forms every DoG level
+//    (gdp_dog_range); ranks > S+3 take no part.  Every rank's GaussPy then ends where the reference
+//    leaves it: worker i with scale i windowed (the other scales untouched), the collector
+//    (collector() == S+3) with the pyramid.  Opt-in because each worker builds a whole pyramid
+//    (no speed-up over one GPU) and its RCCL transport has not yet run on >= S+4 GPUs; ROLES_AUTO
+//    picks it whenever the world has >= S+4 ranks.
+// The collector's pyramid is bit-identical to the reference's collector for EVERY n under either
+// map: GenerateDoG_mpi centres its windows on the integer octave length (`l = float(len-1)/2`,
 // :273 — GDP_CENTRE_INTLEN), while GaussFilter/GenerateDoG use the float-halved centre of
 // :134-143 like GuassDePyramid.h (the two differ only when n is not a multiple of 2^(layer-1),
 // e.g. n = 100; pinned against the reference's own MPI runs, tests/golden/mpi_hashes.json).
 // Repeated calls continue from the current contents, like the reference's in-place methods:
-// every call is collective (every rank builds its band and the collector gathers them).  A rank's
-// band starts from the fused build right after GaussPyInit, from its own rows of the last
-// GenerateDoG_mpi result (re-entry: the op is pointwise, so this equals the collector's whole-
-// pyramid re-entry), or — after single-process calls (GaussFilter / GenerateDoG) or host edits —
-// from its own rows of its whole-image state (gdp_copy_band).  GaussPy is two-way state, as in the
-// reference (GaussDePyramid-MPI.h:18, the float**** every method works on): with `mirror_host`
-// (default) a rank whose GaussPy mirrors its device state (every rank after GaussPyInit and the
-// single-process calls, the collector after GenerateDoG_mpi) uploads it before each mutating call,
-// so edits are processed; a worker's GaussPy is not refreshed by GenerateDoG_mpi (its result rows
-// live in its band context), so it uploads only when the caller sets `host_dirty`.  In the
-// reference the collector's output depends only on the workers' states (scale i from rank i); here
-// on every rank's own rows — the same whenever the ranks hold the same GaussPy (SPMD callers).
-// Role map: with >= S+4 ranks (the reference's own requirement) the class reproduces the
-// reference's roles by default (`roles = ROLES_AUTO`; ROLES_REFERENCE forces them, ROLES_BANDS the
-// band split): rank i < S+3 windows scale i of every octave of its own state (gdp_gauss_scales,
-// integer-length centre) and sends it to rank S+3 (gdp_comm_collect_scales), which forms every DoG
-// level (gdp_dog_range); ranks > S+3 take no part.  Every rank's GaussPy then ends where the
-// reference leaves it: worker i with scale i windowed (the other scales untouched), the collector
-// (collector() == S+3) with the pyramid.  With fewer ranks the band split above runs and the
-// collector is rank 0.
+// every call is collective.  With the band map a rank's band starts from the fused build right
+// after GaussPyInit, from its own rows of the last GenerateDoG_mpi result (re-entry: the op is
+// pointwise, so this equals the collector's whole-pyramid re-entry), or — after single-process
+// calls (GaussFilter / GenerateDoG) or host edits — from its own rows of its whole-image state
+// (gdp_copy_band).  GaussPy is two-way state, as in the reference (GaussDePyramid-MPI.h:18, the
+// float**** every method works on): with `mirror_host` (default) a rank whose GaussPy mirrors its
+// device state (every rank after GaussPyInit and the single-process calls, the collector after
+// GenerateDoG_mpi) uploads it before each mutating call, so edits are processed; a worker's GaussPy
+// is not refreshed by a band GenerateDoG_mpi, so it uploads only when the caller sets `host_dirty`.
+// In the reference the collector's output depends only on the workers' states (scale i from rank
+// i); with the band map on every rank's own rows — the same whenever the ranks hold the same
+// GaussPy (SPMD callers).
 // Differences: MPI is initialised once (if the caller has not) and finalised by the
 // destructor, so GenerateDoG_mpi may be called repeatedly (the reference calls
 // MPI_Init/MPI_Finalize inside and cannot); errors abort with a message instead of continuing.
@@ -88,7 +87,7 @@ public:
     int all_time;
     int rank() const { return rank_; }
     enum { ROLES_AUTO = 0, ROLES_BANDS = 1, ROLES_REFERENCE = 2 };
-    int roles = ROLES_AUTO;  // see the header comment; decided at the first GenerateDoG_mpi
+    int roles = ROLES_BANDS;  // see the header comment; decided at the first GenerateDoG_mpi
     int collector() const { return ref_roles_ ? S + 3 : 0; }  // the rank holding the pyramid
     bool mirror_host = true;  // two-way GaussPy (see the header comment)
     bool host_dirty = false;  // the caller edited GaussPy / data: upload before the next call

@@ -9,6 +9,16 @@
 // 0..S+1, Gaussian S+2) in GaussPy and print the elapsed seconds like the collector rank does
 // (mpitest.cpp:95-96, :171-172).  The reference's MPI fan-out over S+3 worker ranks is replaced by
 // the GPU; the functions can be called repeatedly (no MPI_Init/MPI_Finalize inside).
+// GaussPy is two-way state, as in mpitest.cpp, whose GenerateDoG_* multiply and subtract the
+// GLOBAL GaussPy in place (:50-56, :89, :128-133, :165): a caller that writes GaussPy between
+// GaussPyInit(p) and GenerateDoG_mpi has that edit processed.  With `gdp_mpitest_mirror_host`
+// (default true) every GenerateDoG_* uploads GaussPy first (one H2D DMA of the pinned mirror, or
+// staged row gathers when a caller re-seated a row pointer) and runs the in-place re-entry pass on
+// it; after the call the result is copied back into GaussPy.  With it false the device pyramid is
+// the state: GaussPy is refreshed only after GaussPyInit / GenerateDoG_* / gdp_mpitest_SyncHost(),
+// and edits reach the device only with `gdp_mpitest_host_dirty = true` (the next call uploads first)
+// or gdp_mpitest_SyncDevice().  Only in that mode may a GenerateDoG_* right after GaussPyInit use
+// the fused build (GaussPyInit + GenerateDoG in one pass, bit-identical on unedited contents).
 // Window centre: mpitest.cpp centres on the INTEGER octave length, `l = float(len - 1) / 2.0`
 // (:44, :123), not on GuassDePyramid.h's float-halved length (:107-115); the context uses the same
 // (GDP_CENTRE_INTLEN), so the result equals mpitest.cpp's collector for every n — the two centres
@@ -40,6 +50,8 @@ bool is_initialized = false;
 static gdp_ctx* gdp_mpitest_ctx = nullptr;
 static bool gdp_mpitest_fresh = false;
 static float* gdp_mpitest_host = nullptr;  // pinned device-layout mirror the GaussPy rows point into
+bool gdp_mpitest_mirror_host = true;  // GaussPy two-way: upload before / download after every GenerateDoG_*
+bool gdp_mpitest_host_dirty = false;  // mirror off: the caller edited GaussPy, the next call uploads first
 
 static inline void gdp_mpitest_check(int status, const char* what) {
     if (status != GDP_OK) {
@@ -48,9 +60,39 @@ static inline void gdp_mpitest_check(int status, const char* what) {
     }
 }
 
+// every GaussPy row still where GaussPyInit put it (a caller may re-seat one: the reference's rows
+// are separate new[] arrays, :451-453)
+static inline bool gdp_mpitest_rows_in_mirror() {
+    if (!gdp_mpitest_host) return false;
+    for (int o = 0; o < layer; ++o)
+        for (int s = 0; s < S + 3; ++s) {
+            const float* lev = gdp_mpitest_host + gdp_level_offset(gdp_mpitest_ctx, 0, o, s);
+            const int len = length >> o;
+            for (int r = 0; r < len; ++r)
+                if (GaussPy[o][s][r] != lev + (size_t)r * len) return false;
+        }
+    return true;
+}
+
 static inline int gdp_mpitest_download() {
-    return gdp_mpitest_host ? gdp_download_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
-                            : gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy);
+    return gdp_mpitest_rows_in_mirror() ? gdp_download_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
+                                        : gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy);
+}
+
+// GaussPy (the host pyramid, possibly edited) -> the device pyramid now
+inline void gdp_mpitest_SyncDevice() {
+    if (!is_initialized) return;
+    gdp_mpitest_check(gdp_mpitest_rows_in_mirror()
+                          ? gdp_upload_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
+                          : gdp_upload_pyramid_rows(gdp_mpitest_ctx, 0, (const float* const* const* const*)GaussPy),
+                      "SyncDevice");
+    gdp_mpitest_host_dirty = false;
+    gdp_mpitest_fresh = false;  // the caller's contents now, not necessarily GaussPyInit's
+}
+
+// the device pyramid -> GaussPy now
+inline void gdp_mpitest_SyncHost() {
+    if (is_initialized) gdp_mpitest_check(gdp_mpitest_download(), "SyncHost");
 }
 
 // :438-473 — first call allocates GaussPy (and the device context); every call refills.
@@ -79,12 +121,16 @@ void GaussPyInit(int* data[MAX]) {
     is_initialized = true;
     gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
     gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
-    gdp_mpitest_check(gdp_mpitest_download(), "GaussPyInit");
+    gdp_mpitest_host_dirty = false;  // every level refilled: host edits are overwritten, as in :462-472
     gdp_mpitest_fresh = true;
+    gdp_mpitest_check(gdp_mpitest_download(), "GaussPyInit");
 }
 
 static inline void gdp_mpitest_generate() {
     auto begin = std::chrono::steady_clock::now();
+    // the GLOBAL GaussPy is what the reference's workers multiply and its collector subtracts
+    // (:128-133, :165): upload it first, then the in-place pass on exactly those contents
+    if (gdp_mpitest_mirror_host || gdp_mpitest_host_dirty) gdp_mpitest_SyncDevice();
     gdp_mpitest_check(gdp_mpitest_fresh ? gdp_build(gdp_mpitest_ctx, nullptr) : gdp_generate_dog(gdp_mpitest_ctx, nullptr),
                       "GenerateDoG_mpi");
     gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");

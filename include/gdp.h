@@ -298,8 +298,9 @@ enum {
     GDP_TUNE_BLOCKS_PER_CU = 2, /* value > 0: persistent build grid = CUs x value;
                                    0 (default): one 16x256 tile per block                      */
     GDP_TUNE_GRID = 3,          /* explicit build grid size; 0 (default) = automatic         */
-    GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile shape), 0..18;
-                                   default chosen from the image width                         */
+    GDP_TUNE_VARIANT = 4,       /* build kernel code variant (block size / tile shape): one of
+                                   the ids gdp_build_variants lists (others GDP_ERR_ARG); default
+                                   chosen from the image width and the pyramid backing          */
     GDP_TUNE_TILE_ORDER = 5,    /* build tile order: 0 linear (default), 1 XCD-chunked,
                                    2 XCD row-interleaved                                       */
     GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk,
@@ -341,6 +342,10 @@ enum {
                                       4096 pieces), -1 one piece per image, 0 one hipMalloc */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
+/* The build-kernel variant ids this library holds (GDP_TUNE_VARIANT values): writes up to
+ * `capacity` of them to `ids` (may be NULL) and returns how many there are.  Pure table read: no
+ * device, no context. */
+int gdp_build_variants(int* ids, int capacity);
 /* Benchmark every build-kernel variant x tile order x store mode (GDP_TUNE_ZERO_WINDOW,
  * GDP_TUNE_STORE_PACE) in (0, off) (0, 1) (1, off) (1, 0) on the context's current input (`iters`
  * launches each, HIP events on `stream`) and keep the fastest; reports the variant, tile order

@@ -55,6 +55,23 @@ int gdp_comm_rank(const gdp_comm* comm);
 int gdp_comm_size(const gdp_comm* comm);
 const char* gdp_comm_last_error(const gdp_comm* comm); /* comm may be NULL: last init failure */
 
+/* Failure contract of every collective below (the counterpart of an MPI error on the reference's
+ * per-row MPI_Send / MPI_Recv, GaussDePyramid-MPI.h:285,298).  The transfers of one call are one
+ * ncclGroupStart() .. ncclGroupEnd(); when any ncclSend / ncclRecv inside it fails, the group is
+ * closed before returning (so no later RCCL call of the thread is captured by an open group), the
+ * call returns GDP_ERR_HIP, and the communicator is marked failed: the peers may still wait for
+ * this rank's half of the exchange, so every later collective on it returns GDP_ERR_STATE at
+ * once instead of hanging, and gdp_comm_destroy aborts it (ncclCommAbort) instead of waiting.
+ * gdp_comm_failed: 1 once that happened, 0 before, -1 for NULL. */
+int gdp_comm_failed(const gdp_comm* comm);
+/* Health check, collective over all ranks: a ring exchange (rank r sends 4096 words holding r to
+ * r + 1 and receives r - 1's; a one-rank communicator sends to itself), verified on the host.
+ * GDP_OK when every word arrived; same failure contract as the collectives. stream may be NULL. */
+int gdp_comm_check(gdp_comm* comm, void* stream);
+/* Test hook: the NEXT collective on `comm` adds, first in its group, a send to peer `nranks`
+ * (out of range), which RCCL rejects inside the group — exercises the failure contract above. */
+int gdp_comm_test_inject_fault(gdp_comm* comm);
+
 /* Collective over all ranks of `comm`: every rank passes its band context (built with
  * gdp_band_rows' rows of the same H, W, S, octaves) and image index `band_image`; rank `root`
  * also passes `full`, a whole-image context of the same geometry, whose image `full_image`

@@ -112,6 +112,7 @@ SIGNATURES = {
     "gdp_autotune": (_c_int, [_p, _c_int, _p, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
                               ctypes.POINTER(ctypes.c_float)]),
     "gdp_get_tuning": (_c_int, [_p, _c_int, ctypes.POINTER(_c_int)]),
+    "gdp_build_variants": (_c_int, [ctypes.POINTER(_c_int), _c_int]),
 }
 
 
@@ -148,6 +149,15 @@ def lib():
         raise GdpError(GDP_ERR_STATE, "libgdp ABI version mismatch")
     _lib = L
     return L
+
+
+def build_variants():
+    """The build-kernel variant ids this libgdp.so holds (the values GDP_TUNE_VARIANT accepts)."""
+    L = lib()
+    n = L.gdp_build_variants(None, 0)
+    ids = (_c_int * n)()
+    L.gdp_build_variants(ids, n)
+    return list(ids)
 
 
 def check(status, ctx=None):

@@ -80,6 +80,17 @@ int octaves_for(int n) {
 
 long long round_up(long long v, long long a) { return (v + a - 1) / a * a; }
 
+// Layout / allocation experiment knobs (GDP_SPREAD_CHUNK_MB / _KB, GDP_SPREAD_PHYS_MB,
+// GDP_SPREAD_PERM, GDP_IMAGE_STRIDE_MB, GDP_LEVEL_PAD, GDP_ROWTAP_LAYOUT, GDP_INPUT_VMM: the
+// measurements of DESIGN §4 / §5.1) are read only by a library built with -DGDP_EXPERIMENTS
+// (`make -C csrc exp`, a separate research build); the product library ignores them and runs the
+// measured defaults.  The one product environment switch is GDP_SPREAD_VMM=0 (one hipMalloc).
+#ifdef GDP_EXPERIMENTS
+const char* exp_env(const char* name) { return std::getenv(name); }
+#else
+const char* exp_env(const char*) { return nullptr; }
+#endif
+
 thread_local std::string g_create_error;
 
 }  // namespace
@@ -240,7 +251,7 @@ int launch_build(gdp_ctx* c, hipStream_t st, bool subset = false) {
     // default: one unit per block; GDP_TUNE_GRID / GDP_TUNE_BLOCKS_PER_CU cap it (persistent loop)
     const long long cap = c->grid_override > 0 ? c->grid_override : (c->persistent ? c->blocks_max : units);
     const int grid = (int)std::min<long long>(units, cap);
-    const BuildVariant& v = kVariants[c->variant];
+    const BuildVariant& v = kVariants[variant_index(c->variant)];
     auto kern = (subset ? v.ksub : v.k)[g.L == 5][c->nontemporal ? 1 : 0];
     hipLaunchKernelGGL(kern, dim3(grid), dim3(v.block), (unsigned)c->build_lds, st, c->d_geom, c->d_in, c->d_out,
                        c->d_taps);
@@ -585,7 +596,7 @@ const char* gdp_last_error(const gdp_ctx* ctx) { return ctx ? ctx->err.c_str() :
 static hipError_t alloc_input(gdp_ctx* c, size_t bytes, void** out, gdp_ctx::VmmBuf& vb) {
     bytes = std::max<size_t>(16, bytes);
     *out = nullptr;
-    const char* iv = std::getenv("GDP_INPUT_VMM");
+    const char* iv = exp_env("GDP_INPUT_VMM");
     if (!iv || std::atoi(iv) == 0) return hipMalloc(out, bytes);
     const size_t two = (size_t)2 << 20, span = (bytes + two - 1) / two * two;
     hipMemAllocationProp prop = {};
@@ -662,11 +673,19 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     }
     gran = std::max<size_t>(gran, 256);
     auto up = [gran](size_t v) { return (v + gran - 1) / gran * gran; };
-    const size_t img = up((size_t)c->img_floats * 4);
-    const size_t stride = up(std::max((size_t)g.pyr_stride * 4, img));
+    const char* ck = exp_env("GDP_SPREAD_CHUNK_MB");
+    const char* ckk = exp_env("GDP_SPREAD_CHUNK_KB");
+    // Images stay dense (stride = one image's extent, as with one hipMalloc) unless an experiment
+    // spaces them (GDP_IMAGE_STRIDE_MB) or asks for one piece per image (GDP_SPREAD_CHUNK_MB=0):
+    // only then is the stride rounded to the allocation granularity.  The dense span itself is
+    // rounded up once, so a batch of small images costs at most one granule extra.
+    const bool per_image = (ckk && std::atoll(ckk) <= 0) || (!ckk && ck && std::atoll(ck) <= 0);
+    const size_t dense = (size_t)c->img_floats * 4;
+    const size_t img = per_image ? up(dense) : dense;
+    const size_t stride = (size_t)g.pyr_stride * 4 > dense || per_image ? up(std::max((size_t)g.pyr_stride * 4, img)) : dense;
     g.pyr_stride = (long long)(stride / 4);
-    const size_t span = stride * (size_t)g.batch;
-    const char* ph = std::getenv("GDP_SPREAD_PHYS_MB");
+    const size_t span = up(stride * (size_t)g.batch);
+    const char* ph = exp_env("GDP_SPREAD_PHYS_MB");
     const size_t spacer = ph ? up((size_t)std::max(0ll, std::atoll(ph)) << 20) : 0;
     // default piece: 2 MiB (at most 4096 pieces: larger pyramids take larger pieces).  Measured
     // against one hipMalloc (tools/tune.py A/B, profiles/chunk_*_r04z.log, vmm_*_r04y.log): 4096^2
@@ -674,15 +693,13 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     // and equal on another, 64 x 4096^2 within 1 %; 512 MiB+ pieces behave like one allocation.
     // GDP_SPREAD_CHUNK_MB = n MiB pieces, 0 = one piece per image.
     // (GDP_SPREAD_CHUNK_KB: the same in KiB — below 2 MiB only for measurement: 37-62 % of 8 TB/s)
-    const char* ck = std::getenv("GDP_SPREAD_CHUNK_MB");
-    const char* ckk = std::getenv("GDP_SPREAD_CHUNK_KB");
     const size_t two = (size_t)2 << 20;
     const size_t fixed = ckk ? (std::atoll(ckk) > 0 ? up((size_t)std::atoll(ckk) << 10) : 0)
                        : ck  ? (std::atoll(ck) > 0 ? up((size_t)std::atoll(ck) << 20) : 0)
                              : up(std::max(two, (span / 4096 + two - 1) / two * two));
     // the pieces to map: [off, off + bytes)
     std::vector<std::pair<size_t, size_t>> pieces;
-    if (fixed && stride == img) {
+    if (fixed && stride == img) {  // dense images: fixed pieces tiling the (granule-rounded) span
         for (size_t off = 0; off < span; off += fixed) pieces.push_back({off, std::min(fixed, span - off)});
         c->pyr_chunk_kb = (int)(fixed >> 10);
     } else {
@@ -710,7 +727,7 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     // 9, ..), 2 last piece first.  The random order makes the rate insensitive to the tile order:
     // 64 x 4096^2 v16 linear 4.78 vs 5.17 ms (best 4.733 vs 4.770), 64 x 1080x1920 v17 linear
     // 0.601 vs 0.689 (best equal), 4096^2 equal, 16384^2 -0.1..-0.7 % (rperm_*_r04a{h,i}.log)
-    const char* pm = std::getenv("GDP_SPREAD_PERM");
+    const char* pm = exp_env("GDP_SPREAD_PERM");
     const int perm = pm ? std::atoi(pm) : 3;
     const size_t np = pieces.size();
     std::vector<size_t> shuffled;
@@ -799,7 +816,9 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     };
     try {
     c->device = device;
-    c->variant = default_variant(W, (long long)(row_end - row_begin) * W, batch);
+    const char* vm = std::getenv("GDP_SPREAD_VMM");  // "0": the pyramid in one hipMalloc
+    const bool want_vmm = !vm || std::atoi(vm) != 0;
+    c->variant = default_variant(W, want_vmm);  // revised below if the chunked backing is refused
     // in-place re-entry pass (GenerateDoG on the current contents): 64-thread blocks stream best on
     // single images (4096^2 0.148 vs 0.152 ms for 256 threads, 16384^2 2.37 vs 2.49;
     // profiles/ab_sub_c*_r03m.log), 256-thread blocks on small batches, 1024-thread above
@@ -840,14 +859,14 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     c->in_img_stride_own = g.in_img_stride;
 
     // optional padding between levels (floats, multiple of 64) — layout experiment knob
-    const char* pad_env = std::getenv("GDP_LEVEL_PAD");
+    const char* pad_env = exp_env("GDP_LEVEL_PAD");
     const long long level_pad = pad_env ? round_up(std::max(0ll, std::atoll(pad_env)), kLevelAlign) : 0;
     // Row-window layout of a non-square image: [row][scale] (default) or, with GDP_ROWTAP_LAYOUT=0,
     // [scale][row].  A tile's rows then read their S+3 windows from ~L/32 lines per row instead of
     // one cold line per scale: 65536 x 4096 builds in 1.227 vs 1.43-1.46 ms (v15), 16384 x 4096 in
     // 0.315 vs 0.363 ms — the speed of row windows that are always hot (timing-only build, 1.25
     // ms); config 3 and the in-place passes unchanged (profiles/ab_rowtap_r03c.log, bit-exact)
-    const char* rl_env = std::getenv("GDP_ROWTAP_LAYOUT");
+    const char* rl_env = exp_env("GDP_ROWTAP_LAYOUT");
     const bool rowtap_interleave = rl_env ? std::atoi(rl_env) != 0 : true;
     // tap table: per octave, column taps [L][round4(W_o)] then row taps [L][round4(H_o)] (global rows)
     long long tap_off = 0, lev_off = 0, grp = 0;
@@ -899,7 +918,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     c->img_floats = g.pyr_stride;
     // optional image stride (MiB) — layout experiment knob, like GDP_LEVEL_PAD: images that far
     // apart, so tile order 1's eight XCD ranges (batch / 8 images each) start 8 x stride apart
-    if (const char* is_env = std::getenv("GDP_IMAGE_STRIDE_MB"))
+    if (const char* is_env = exp_env("GDP_IMAGE_STRIDE_MB"))
         g.pyr_stride = std::max(g.pyr_stride, round_up(std::max(0ll, std::atoll(is_env)) << 18, kLevelAlign));
     const long long tail_per_img = (g.F < O) ? grp - g.oct[g.F].grp_begin : 0;
     const long long tail_units = (tail_per_img * batch + kTailGroups - 1) / kTailGroups;
@@ -915,7 +934,11 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // the XCD-chunked order; with the default v15 the linear order is the faster one on 16384^2,
     // 1.344 vs 1.375 ms, and batches differ box to box — gdp_autotune measures both.)
     g.tile_order = 0;
-    retile(c, kVariants[c->variant].tile_cols, kVariants[c->variant].tile_rows);
+    if (retile(c, kVariants[variant_index(c->variant)].tile_cols, kVariants[variant_index(c->variant)].tile_rows) != GDP_OK) {
+        const std::string m = c->err;
+        drop();
+        return fail(GDP_ERR_ARG, m);
+    }
     conv_sweep_geom(c);
     c->h_taps.assign((size_t)tap_off, 0.0f);
     fill_host_taps(c, c->centre_mode);
@@ -959,24 +982,31 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // The pyramid: separately created physical pieces mapped into one address range (alloc_spread;
     // default), or one hipMalloc (GDP_SPREAD_VMM=0, or when the VMM calls are refused).
     bool pyr_done = false;
-    const char* vm = std::getenv("GDP_SPREAD_VMM");
-    if (!vm || std::atoi(vm) != 0) {
+    if (want_vmm) {
         std::string where;
+        const long long stride0 = g.pyr_stride;
         if ((e = alloc_spread(c, where)) == hipSuccess) {
             pyr_done = true;
         } else if (vm) {
             return hip_fail(e, ("spread pyramid (GDP_SPREAD_VMM, " + where + ")").c_str());
         } else {
             free_pyramid(c);  // not asked for explicitly: one hipMalloc instead
+            g.pyr_stride = stride0;  // alloc_spread may have rounded it
             (void)hipGetLastError();
         }
     }
-    if (!pyr_done && (e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
-        return hip_fail(e, "hipMalloc(pyramid)");
-    // On the chunked backing v11's tile runs faster in its flattened form v17 (same 8 x 384 tile,
-    // same geometry): 64 x 1080x1920 0.637 vs 0.698 ms with the default store modes
-    // (profiles/defvar_c3_r04am.log); on one hipMalloc v11 stays ahead (0.68-0.69 vs 0.78)
-    if (pyr_done && c->variant == 11) c->variant = 17;
+    if (!pyr_done) {
+        if ((e = hipMalloc(&c->d_out_own, std::max<size_t>(16, (size_t)g.pyr_stride * batch * 4))) != hipSuccess)
+            return hip_fail(e, "hipMalloc(pyramid)");
+        if (want_vmm) {  // the chunked backing was refused: the default for one allocation
+            c->variant = default_variant(W, false);
+            if (retile(c, kVariants[variant_index(c->variant)].tile_cols, kVariants[variant_index(c->variant)].tile_rows) != GDP_OK) {
+                const std::string m = c->err;
+                drop();
+                return fail(GDP_ERR_ARG, m);
+            }
+        }
+    }
     c->d_out = c->d_out_own;
     if ((e = hipMalloc(&c->d_sum, sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(sum)");
     c->d_in = c->d_in_own;
@@ -1878,7 +1908,8 @@ int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* be
         int rc = gdp_set_tuning(c, GDP_TUNE_ZERO_WINDOW, zw);
         if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_STORE_PACE, sp);
         if (rc != GDP_OK) return rc;
-        for (int v = 0; v < kNumVariants; ++v) {
+        for (const BuildVariant& bvar : kVariants) {
+            const int v = bvar.id;
             for (int ord = 0; ord <= 1; ++ord) {
                 rc = gdp_set_tuning(c, GDP_TUNE_VARIANT, v);
                 if (rc == GDP_OK) rc = gdp_set_tuning(c, GDP_TUNE_TILE_ORDER, ord);
@@ -1908,6 +1939,11 @@ int gdp_autotune(gdp_ctx* c, int iters, void* stream, int* best_variant, int* be
     if (best_ms) *best_ms = bt / iters;
     return GDP_OK;
 } GDP_ABI_CATCH(c)
+
+int gdp_build_variants(int* ids, int capacity) {
+    for (int i = 0; i < kNumVariants && i < capacity && ids; ++i) ids[i] = kVariants[i].id;
+    return kNumVariants;
+}
 
 int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
     if (!c || !value) return GDP_ERR_ARG;
@@ -2020,14 +2056,15 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             c->geom.tile_order = value;
             return upload_geom(c);
         case GDP_TUNE_VARIANT: {
-            if (value < 0 || value >= kNumVariants) return c->status(GDP_ERR_ARG, "variant out of range");
+            const int vi = variant_index(value);
+            if (vi < 0) return c->status(GDP_ERR_ARG, "build variant %d is not built (gdp_build_variants lists them)", value);
             const int old = c->variant;
             c->variant = value;
-            int rc = retile(c, kVariants[value].tile_cols, kVariants[value].tile_rows);
+            int rc = retile(c, kVariants[vi].tile_cols, kVariants[vi].tile_rows);
             if (rc == GDP_OK) rc = upload_geom(c);
             if (rc != GDP_OK) {
                 c->variant = old;
-                retile(c, kVariants[old].tile_cols, kVariants[old].tile_rows);
+                retile(c, kVariants[variant_index(old)].tile_cols, kVariants[variant_index(old)].tile_rows);
             }
             return rc;
         }

@@ -17,6 +17,12 @@
 struct gdp_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    // A grouped transfer failed: the group was closed (ncclGroupEnd) but the peers may still wait
+    // for this rank's half of it, so the communicator is unusable — every later collective on it
+    // returns GDP_ERR_STATE at once, and gdp_comm_destroy aborts it instead of a (possibly
+    // blocking) ncclCommDestroy.
+    bool failed = false;
+    int inject = 0;  // gdp_comm_test_inject_fault: the next group adds a send to an invalid peer
     std::string err;
 };
 
@@ -31,16 +37,53 @@ int fail(gdp_comm* c, int code, const std::string& m) {
     return code;
 }
 
-#define GDP_NCCL(c, call)                                                                                 \
+// Inside ncclGroupStart() .. ncclGroupEnd(): a failing ncclSend / ncclRecv must still close the
+// group, or every later RCCL call of this thread is swallowed by the open group.
+#define GDP_NCCL_IN_GROUP(c, call)                                                                        \
     do {                                                                                                  \
         ncclResult_t r_ = (call);                                                                         \
-        if (r_ != ncclSuccess) return fail((c), GDP_ERR_HIP, std::string(#call ": ") + ncclGetErrorString(r_)); \
+        if (r_ != ncclSuccess) return group_fail((c), std::string(#call ": ") + ncclGetErrorString(r_));   \
     } while (0)
 #define GDP_HIPC(c, call)                                                                                 \
     do {                                                                                                  \
         hipError_t e_ = (call);                                                                           \
         if (e_ != hipSuccess) return fail((c), GDP_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
     } while (0)
+
+// Close the open group after a failed transfer and mark the communicator failed.
+int group_fail(gdp_comm* c, const std::string& m) {
+    const ncclResult_t e = ncclGroupEnd();
+    c->failed = true;
+    return fail(c, GDP_ERR_HIP, m + (e == ncclSuccess ? "" : std::string("; ncclGroupEnd: ") + ncclGetErrorString(e)) +
+                                    " (group closed; communicator marked failed)");
+}
+// Entry check of every collective: a communicator that failed earlier is refused, never reused.
+int refuse_failed(gdp_comm* c, const char* who) {
+    return fail(c, GDP_ERR_STATE, std::string(who) + ": an earlier collective on this communicator failed ("
+                                      + c->err + "); destroy it and create a new one");
+}
+// Open a group; with a test fault armed, its first transfer targets peer `nranks` (invalid).
+int group_start(gdp_comm* c, hipStream_t st) {
+    const ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) {
+        c->failed = true;
+        return fail(c, GDP_ERR_HIP, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+    }
+    if (c->inject) {
+        c->inject = 0;
+        static float dummy_dev_ptr_unused;  // never dereferenced: RCCL rejects the peer first
+        GDP_NCCL_IN_GROUP(c, ncclSend(&dummy_dev_ptr_unused, 1, ncclFloat, c->nranks, c->comm, st));
+    }
+    return GDP_OK;
+}
+int group_end(gdp_comm* c) {
+    const ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) {
+        c->failed = true;
+        return fail(c, GDP_ERR_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(r) + " (communicator marked failed)");
+    }
+    return GDP_OK;
+}
 
 int band_align(int octaves) { return 1 << (std::max(octaves, 5) - 1); }
 
@@ -184,9 +227,52 @@ int gdp_comm_init(gdp_comm** out, const unsigned char id[GDP_COMM_ID_BYTES], int
 
 void gdp_comm_destroy(gdp_comm* c) {
     if (!c) return;
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    // a failed communicator may have operations its peers never matched: abort, do not wait
+    if (c->comm) (void)(c->failed ? ncclCommAbort(c->comm) : ncclCommDestroy(c->comm));
     delete c;
 }
+
+int gdp_comm_failed(const gdp_comm* c) { return c ? (c->failed ? 1 : 0) : -1; }
+
+int gdp_comm_test_inject_fault(gdp_comm* c) try {
+    if (!c) return GDP_ERR_ARG;
+    c->inject = 1;
+    return GDP_OK;
+} GDP_COMM_CATCH(c)
+
+int gdp_comm_check(gdp_comm* c, void* stream) try {
+    // ring: rank r sends kWords words of r to (r + 1) % n and receives (r - 1 + n) % n's; with one
+    // rank that is a send to itself.  Verified on the host.
+    if (!c) return GDP_ERR_ARG;
+    if (c->failed) return refuse_failed(c, "gdp_comm_check");
+    constexpr size_t kWords = 4096;
+    GDP_HIPC(c, hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    int* d = nullptr;
+    GDP_HIPC(c, hipMalloc(&d, 2 * kWords * sizeof(int)));
+    std::vector<int> h(kWords, c->rank);
+    int rc = GDP_OK;
+    auto step = [&]() -> int {
+        GDP_HIPC(c, hipMemcpyAsync(d, h.data(), kWords * sizeof(int), hipMemcpyHostToDevice, st));
+        GDP_HIPC(c, hipMemsetAsync(d + kWords, 0xff, kWords * sizeof(int), st));
+        const int next = (c->rank + 1) % c->nranks, prev = (c->rank + c->nranks - 1) % c->nranks;
+        int r = group_start(c, st);
+        if (r != GDP_OK) return r;
+        GDP_NCCL_IN_GROUP(c, ncclSend(d, kWords, ncclInt32, next, c->comm, st));
+        GDP_NCCL_IN_GROUP(c, ncclRecv(d + kWords, kWords, ncclInt32, prev, c->comm, st));
+        if ((r = group_end(c)) != GDP_OK) return r;
+        GDP_HIPC(c, hipMemcpyAsync(h.data(), d + kWords, kWords * sizeof(int), hipMemcpyDeviceToHost, st));
+        GDP_HIPC(c, hipStreamSynchronize(st));
+        for (size_t k = 0; k < kWords; ++k)
+            if (h[k] != prev)
+                return fail(c, GDP_ERR_STATE, "gdp_comm_check: word " + std::to_string(k) + " from rank " +
+                                                  std::to_string(prev) + " reads " + std::to_string(h[k]));
+        return GDP_OK;
+    };
+    rc = step();
+    (void)hipFree(d);
+    return rc;
+} GDP_COMM_CATCH(c)
 
 int gdp_comm_rank(const gdp_comm* c) { return c ? c->rank : -1; }
 int gdp_comm_size(const gdp_comm* c) { return c ? c->nranks : -1; }
@@ -209,6 +295,7 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
     // band == NULL: this rank's band is empty (more ranks than aligned row bands); it sends nothing
     if (!c || root < 0 || root >= c->nranks || (c->rank == root && !full))
         return fail(c, GDP_ERR_ARG, "gdp_comm_gather_bands: bad argument");
+    if (c->failed) return refuse_failed(c, "gdp_comm_gather_bands");
     int H, W, S, O, B;
     if (gdp_get_geometry(band ? band : full, &H, &W, &S, &O, &B) != GDP_OK) {
         if (band || c->rank == root) return fail(c, GDP_ERR_ARG, "band geometry");
@@ -234,17 +321,19 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
                 return fail(c, GDP_ERR_ARG, "band context rows differ from gdp_band_rows' band of this rank");
         }
     }
-    GDP_NCCL(c, ncclGroupStart());
+    int rc = group_start(c, st);
+    if (rc != GDP_OK) return rc;
     for (const gdp_transfer& t : plan) {
         const size_t n = (size_t)t.rows * t.cols;
         if (t.kind == GDP_XFER_SEND)
-            GDP_NCCL(c, ncclSend(gdp_device_level(band, band_image, t.octave, t.scale), n, ncclFloat, t.peer, c->comm, st));
+            GDP_NCCL_IN_GROUP(c, ncclSend(gdp_device_level(band, band_image, t.octave, t.scale), n, ncclFloat, t.peer,
+                                          c->comm, st));
         else if (t.kind == GDP_XFER_RECV)
-            GDP_NCCL(c, ncclRecv(const_cast<float*>(gdp_device_level(full, full_image, t.octave, t.scale)) +
-                                     (size_t)t.first_row * t.cols,
-                                 n, ncclFloat, t.peer, c->comm, st));
+            GDP_NCCL_IN_GROUP(c, ncclRecv(const_cast<float*>(gdp_device_level(full, full_image, t.octave, t.scale)) +
+                                              (size_t)t.first_row * t.cols,
+                                          n, ncclFloat, t.peer, c->comm, st));
     }
-    GDP_NCCL(c, ncclGroupEnd());
+    if ((rc = group_end(c)) != GDP_OK) return rc;
     for (const gdp_transfer& t : plan) {  // the collector's own band: device-to-device copies
         if (t.kind != GDP_XFER_COPY || !band) continue;
         float* dst = const_cast<float*>(gdp_device_level(full, full_image, t.octave, t.scale)) + (size_t)t.first_row * t.cols;
@@ -269,6 +358,7 @@ int gdp_comm_scale_plan(int S, int O, int nranks, int rank, gdp_scale_transfer* 
 
 int gdp_comm_collect_scales(gdp_comm* c, gdp_ctx* ctx, int image, void* stream) try {
     if (!c || !ctx) return fail(c, GDP_ERR_ARG, "gdp_comm_collect_scales: bad argument");
+    if (c->failed) return refuse_failed(c, "gdp_comm_collect_scales");
     int H, W, S, O, B;
     if (gdp_get_geometry(ctx, &H, &W, &S, &O, &B) != GDP_OK || image < 0 || image >= B)
         return fail(c, GDP_ERR_ARG, "gdp_comm_collect_scales: bad context / image");
@@ -281,7 +371,8 @@ int gdp_comm_collect_scales(gdp_comm* c, gdp_ctx* ctx, int image, void* stream) 
     if (plan.empty()) return GDP_OK;  // ranks > S+3 take no part (GaussDePyramid-MPI.h:269-335)
     GDP_HIPC(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)gdp_stream(ctx);
-    GDP_NCCL(c, ncclGroupStart());
+    int rc = group_start(c, st);
+    if (rc != GDP_OK) return rc;
     for (const gdp_scale_transfer& t : plan) {
         int rows, cols, first;
         gdp_level_dims(ctx, t.octave, &rows, &cols, &first);
@@ -289,11 +380,11 @@ int gdp_comm_collect_scales(gdp_comm* c, gdp_ctx* ctx, int image, void* stream) 
         if (n == 0) continue;
         float* lev = const_cast<float*>(gdp_device_level(ctx, image, t.octave, t.scale));
         if (t.kind == GDP_SCALE_SEND)
-            GDP_NCCL(c, ncclSend(lev, n, ncclFloat, t.peer, c->comm, st));
+            GDP_NCCL_IN_GROUP(c, ncclSend(lev, n, ncclFloat, t.peer, c->comm, st));
         else
-            GDP_NCCL(c, ncclRecv(lev, n, ncclFloat, t.peer, c->comm, st));
+            GDP_NCCL_IN_GROUP(c, ncclRecv(lev, n, ncclFloat, t.peer, c->comm, st));
     }
-    GDP_NCCL(c, ncclGroupEnd());
+    if ((rc = group_end(c)) != GDP_OK) return rc;
     GDP_HIPC(c, hipStreamSynchronize(st));
     return GDP_OK;
 } GDP_COMM_CATCH(c)
@@ -312,6 +403,7 @@ int gdp_comm_halo_plan(int H, int nranks, int rank, int O, gdp_halo_transfer* ou
 
 int gdp_comm_exchange_halo(gdp_comm* c, gdp_ctx* band, void* stream) try {
     if (!c) return GDP_ERR_ARG;
+    if (c->failed) return refuse_failed(c, "gdp_comm_exchange_halo");
     if (!band) return GDP_OK;  // empty band: its neighbours do not count it as one
     int H, W, S, O, B;
     if (gdp_get_geometry(band, &H, &W, &S, &O, &B) != GDP_OK) return fail(c, GDP_ERR_ARG, "band geometry");
@@ -341,24 +433,24 @@ int gdp_comm_exchange_halo(gdp_comm* c, gdp_ctx* band, void* stream) try {
             return fail(c, GDP_ERR_ARG, "band input pitch differs from its halo rows' (bind an input of pitch round_up(W, 4))");
     }
     const ncclDataType_t ty = u8 ? ncclUint8 : ncclInt32;
-    GDP_NCCL(c, ncclGroupStart());
+    int rc = group_start(c, st);
+    if (rc != GDP_OK) return rc;
     for (int b = 0; b < B; ++b) {
         const char* in = static_cast<const char*>(inputs[(size_t)b].first);
         const size_t pitch = inputs[(size_t)b].second;
         for (const gdp_halo_transfer& t : plan) {
             const size_t n = (size_t)t.rows * pitch;  // whole padded rows (the same pitch on both sides)
             if (t.kind == GDP_HALO_SEND) {
-                GDP_NCCL(c, ncclSend(in + (size_t)t.first_row * pitch * esz, n, ty, t.peer, c->comm, st));
+                GDP_NCCL_IN_GROUP(c, ncclSend(in + (size_t)t.first_row * pitch * esz, n, ty, t.peer, c->comm, st));
             } else {
                 const int side = t.kind == GDP_HALO_RECV_ABOVE ? 0 : 1;
                 const size_t rows_side = side ? (size_t)nb : (size_t)na;
-                GDP_NCCL(c, ncclRecv(static_cast<char*>(halo[side]) + (size_t)b * rows_side * hpitch[side] * esz, n, ty,
-                                     t.peer, c->comm, st));
+                GDP_NCCL_IN_GROUP(c, ncclRecv(static_cast<char*>(halo[side]) + (size_t)b * rows_side * hpitch[side] * esz, n,
+                                              ty, t.peer, c->comm, st));
             }
         }
     }
-    GDP_NCCL(c, ncclGroupEnd());
-    return GDP_OK;
+    return group_end(c);
 } GDP_COMM_CATCH(c)
 
 }  // extern "C"

@@ -35,6 +35,24 @@ def test_python_signatures_cover_header(pkg):
     assert set(SIGNATURES) == set(pkg.header_functions())
 
 
+def test_build_variant_table(pkg):
+    """The variant ids the library holds (gdp_build_variants, a pure table read) are the round-5
+    kept set; the library is the stripped product build (no experiment or timing-only code)."""
+    from conftest import BUILD_VARIANTS
+
+    assert tuple(pkg.build_variants()) == BUILD_VARIANTS
+    assert pkg.lib().gdp_build_variants(None, 0) == len(BUILD_VARIANTS)
+    lib_dir = os.path.join(PKG, "lib")
+    assert sorted(f for f in os.listdir(lib_dir) if f.endswith(".so")) == ["libgdp.so", "libgdp_comm.so"]
+    # the experiment knobs are compiled out of the product library (GDP_EXPERIMENTS builds only)
+    with open(os.path.join(lib_dir, "libgdp.so"), "rb") as f:
+        blob = f.read()
+    for knob in (b"GDP_SPREAD_PHYS_MB", b"GDP_SPREAD_CHUNK_KB", b"GDP_LEVEL_PAD", b"GDP_INPUT_VMM",
+                 b"GDP_IMAGE_STRIDE_MB", b"GDP_SPREAD_PERM", b"GDP_ROWTAP_LAYOUT"):
+        assert knob not in blob, knob
+    assert b"GDP_SPREAD_VMM" in blob  # the one product switch (one hipMalloc, INTEGRATION.md §5)
+
+
 def test_host_only_entry_points(pkg):
     L = pkg.lib()
     for n, want in [(1, 1), (2, 2), (512, 10), (513, 10), (4096, 13), (0, 0)]:
@@ -110,7 +128,7 @@ def test_comm_library_exports_its_header(pkg):
     pkg.lib()  # torch first, then libgdp (the comm library links both)
     L = _comm_lib()
     names = pkg.header_functions(os.path.join(REPO, "include", "gdp_comm.h"))
-    assert len(names) == 13
+    assert len(names) == 16  # + gdp_comm_failed, gdp_comm_check, gdp_comm_test_inject_fault (round 5)
     for n in names:
         assert hasattr(L, n), n
 

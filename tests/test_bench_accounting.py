@@ -4,6 +4,7 @@ import os
 import sys
 
 import pytest
+from conftest import BUILD_VARIANTS
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -210,7 +211,7 @@ def test_traffic_records_match_only_their_kernel_instance():
     import bench
 
     for cfg in ("c2", "c3", "c4", "c5"):
-        for v in range(30):  # every variant the autotune can pick (19-29: contiguous spans, round 4)
+        for v in BUILD_VARIANTS:  # every variant the autotune can pick (20, 23, 27: contiguous spans)
             for t in (0, 1):
                 for zw in (0, 1):  # the autotune also picks GDP_TUNE_ZERO_WINDOW
                     rec = bench.latest_pmc(cfg, v, t, zero_window=zw)
@@ -221,7 +222,7 @@ def test_traffic_records_match_only_their_kernel_instance():
                     assert 0.99 < rec["kernel_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < \
                         (1.12 if v >= 19 else 1.05), (cfg, v, t, zw)
     for n in (2, 4, 8):  # config 5 at N > 1: rank 0's band of N
-        for v in range(30):
+        for v in BUILD_VARIANTS:
             for t in (0, 1):
                 for zw in (0, 1):
                     rec = bench.latest_pmc("c5", v, t, zero_window=zw, band_of=n)

@@ -10,6 +10,7 @@ import subprocess
 
 import numpy as np
 import pytest
+from conftest import BUILD_VARIANTS
 
 pytestmark = pytest.mark.gpu
 
@@ -57,38 +58,44 @@ def test_device_taps_are_the_reference_taps(pkg, golden):
 
 
 @pytest.mark.parametrize("H,W,O,band", [(1080, 1920, 5, None), (300, 37, 0, None), (4096, 256, 5, (1024, 2048))])
-def test_row_window_layouts_agree(pkg, oracle, monkeypatch, H, W, O, band):
-    """Non-square images keep their row windows [row][scale] (default since round 3: a tile's rows
-    read their S+3 windows from a few lines instead of one cold line per scale) or, with
-    GDP_ROWTAP_LAYOUT=0, [scale][row].  Both give the oracle's bits in the fused build, the
-    in-place re-entry, the window pass and the subset build, and the same device taps."""
+def test_nonsquare_row_windows(pkg, oracle, H, W, O, band):
+    """Non-square images keep their row windows [row][scale] (a tile's rows read their S+3
+    windows from a few lines instead of one cold line per scale): the fused build, the in-place
+    re-entry, the window pass and the subset build give the oracle's bits, and a row band the
+    whole image's rows.  (The [scale][row] alternative is a GDP_EXPERIMENTS-only layout since
+    round 5.)"""
     img = oracle.lcg_image(H, W, 77 + H)
     r0, r1 = band or (0, H)
     kw = dict(row_begin=r0, row_end=r1) if band else {}
-    got = {}
-    for lay in ("0", "1"):
-        monkeypatch.setenv("GDP_ROWTAP_LAYOUT", lay)
-        with pkg.PyramidContext(H, W, S=2, octaves=O, **kw) as ctx:
-            ctx.set_input(img[r0:r1])
-            ctx.build()
-            ctx.generate_dog()
-            ctx.gauss_range(0, ctx.O)
-            ctx.sync()
-            got[lay] = (ctx.pyramid(0), [ctx.taps(1, o, s) for o in range(ctx.O) for s in range(5)])
-            ctx.build_subset()
-            ctx.sync()
-            got[lay] += (ctx.pyramid(0),)
-    _assert_same(got["0"][0], got["1"][0], ("layouts", H, W))
-    _assert_same(got["0"][2], got["1"][2], ("subset layouts", H, W))
-    for a, b in zip(got["0"][1], got["1"][1]):
-        _assert_same(a, b, ("taps", H, W))
+    with pkg.PyramidContext(H, W, S=2, octaves=O, **kw) as ctx:
+        ctx.set_input(img[r0:r1])
+        ctx.build()
+        ctx.generate_dog()
+        ctx.gauss_range(0, ctx.O)
+        ctx.sync()
+        got = ctx.pyramid(0) if band is None else [ctx.level(0, o, s) for o in range(ctx.O) for s in range(5)]
+        dims = [ctx.level_dims(o) for o in range(ctx.O)]
+        for o in range(ctx.O):
+            for s in range(5):
+                _assert_same(ctx.taps(1, o, s), oracle.taps(H, o, s), ("row taps", H, W, o, s))
+        ctx.set_window_centre("intlen")  # the AVX-512 header's subset centres on the integer length
+        ctx.build_subset()
+        ctx.sync()
+        sub = ctx.pyramid(0) if band is None else None
+    Oo = O or oracle.default_octaves(H, W)
+    want = oracle.build_pyramid(img, 2, O or None)
+    oracle.generate_dog(want, H, W, 2, Oo)
+    for o in range(Oo):
+        oracle.gauss_octave(want, H, W, 2, o)
     if band is None:
-        want = oracle.build_pyramid(img, 2, O or None)
-        Oo = O or oracle.default_octaves(H, W)
-        oracle.generate_dog(want, H, W, 2, Oo)
+        _assert_same(got, want, ("oracle", H, W))
+        _assert_same(sub, oracle.subset_a512omp(oracle.init_pyramid(img, 2, O or None), H, W, 2, Oo), ("subset", H, W))
+    else:
+        lv = oracle.levels(want, H, W, 2, Oo)
         for o in range(Oo):
-            oracle.gauss_octave(want, H, W, 2, o)
-        _assert_same(got["1"][0], want, ("oracle", H, W))
+            rows, _, first = dims[o]
+            for s in range(5):
+                _assert_same(got[o * 5 + s], lv[(o, s)][first:first + rows], ("band", H, W, o, s))
 
 
 # ------------------------------------------------------------------ full builds vs reference
@@ -147,10 +154,10 @@ def test_build_matches_oracle_shapes(pkg, oracle, H, W, S, O):
     _assert_same(_gpu_pyramid(pkg, img, S, O), want, (H, W, S, O))
 
 
-@pytest.mark.parametrize("variant", range(30))
+@pytest.mark.parametrize("variant", BUILD_VARIANTS)
 def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
     """Every code variant of the build kernel (block size / tile width / octave-0 path, the
-    contiguous-span units of variants 19-29 (27-29 source-aligned), also persistent grids and plain stores) produces
+    contiguous-span units of variants 20 / 23 (27 source-aligned), also persistent grids and plain stores) produces
     identical bits — including widths that are not a multiple of 4 (spans then cut inside a row's
     ragged last group) and row bands."""
     for H, W, S, O in [(100, 300, 2, 0), (67, 1000, 3, 5), (256, 512, 2, 9), (33, 65, 1, 0), (128, 1024, 2, 5),
@@ -181,44 +188,41 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
                         _assert_same(ctx.level(b, o, s), lv, ("band", variant, H, W, r0, r1, b, o, s))
 
 
-@pytest.mark.parametrize("env", [{"GDP_IMAGE_STRIDE_MB": "3"},
-                                 {"GDP_SPREAD_VMM": "1"},
-                                 {"GDP_SPREAD_VMM": "1", "GDP_IMAGE_STRIDE_MB": "5"},
-                                 {"GDP_SPREAD_VMM": "1", "GDP_SPREAD_PHYS_MB": "4"},
-                                 {"GDP_SPREAD_VMM": "1", "GDP_SPREAD_CHUNK_MB": "2"},
-                                 {"GDP_INPUT_VMM": "1"}, {"GDP_SPREAD_PERM": "1"}, {"GDP_SPREAD_PERM": "2"},
-                                 {"GDP_SPREAD_PERM": "0"}])
-def test_spread_image_stride_is_bit_exact(pkg, oracle, monkeypatch, env):
-    """The spread layouts (the XCD-range placement experiment, DESIGN §5.1: GDP_IMAGE_STRIDE_MB,
-    and the reserved-range form GDP_SPREAD_VMM with GDP_SPREAD_PHYS_MB physical spacers) only move
-    images apart: every image, level, checksum and raw device-layout copy equals the dense
-    layout's, in both tile orders."""
+@pytest.mark.parametrize("H,W,B", [(300, 500, 3), (64, 64, 7), (1080, 1920, 2)])
+def test_chunked_backing_is_dense_and_bit_exact(pkg, oracle, monkeypatch, H, W, B):
+    """The default backing (2 MiB physical pieces in one reserved range) keeps the images DENSE:
+    gdp_pyramid_bytes is the batch's exact extent (no per-image rounding to the allocation
+    granularity), and every image, level, checksum and raw device-layout copy equals
+    the one-hipMalloc context's, in both tile orders."""
     import ctypes
-    H, W, B = 300, 500, 3
     imgs = [oracle.lcg_image(H, W, 40 + b) for b in range(B)]
+    monkeypatch.setenv("GDP_SPREAD_VMM", "0")
     with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as dense:
+        assert dense.tuning()["pyramid_chunk_kb"] == 0
         for b, im in enumerate(imgs):
             dense.set_input(im, b)
         dense.build()
         sums = [dense.checksum(b) for b in range(B)]
         n = pkg.lib().gdp_image_floats(dense._ctx)
+        dense_bytes = pkg.lib().gdp_pyramid_bytes(dense._ctx)
         raw = np.empty((B, n), np.float32)
         for b in range(B):
             assert pkg.lib().gdp_download_image_raw(dense._ctx, b, raw[b].ctypes.data_as(ctypes.c_void_p)) == 0
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("GDP_SPREAD_VMM")
     with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as ctx:
+        assert ctx.tuning()["pyramid_chunk_kb"] > 0
         assert pkg.lib().gdp_image_floats(ctx._ctx) == n
+        assert pkg.lib().gdp_pyramid_bytes(ctx._ctx) == dense_bytes == n * B * 4
         for b, im in enumerate(imgs):
             ctx.set_input(im, b)
         for order in (0, 1):
             ctx.set_tuning(variant=0, tile_order=order)
             ctx.build()
             for b, im in enumerate(imgs):
-                _assert_same(ctx.pyramid(b), oracle.build_pyramid(im, 2, 5), ("stride", env, order, b))
+                _assert_same(ctx.pyramid(b), oracle.build_pyramid(im, 2, 5), ("chunked", order, b))
                 assert ctx.checksum(b) == sums[b]
         got = np.empty(n, np.float32)
-        for b in range(B):  # raw copies cover the dense extent only (the gaps may be unmapped)
+        for b in range(B):
             assert pkg.lib().gdp_download_image_raw(ctx._ctx, b, got.ctypes.data_as(ctypes.c_void_p)) == 0
             assert np.array_equal(got.view(np.uint32), raw[b].view(np.uint32))
         assert pkg.lib().gdp_upload_image_raw(ctx._ctx, 1, raw[0].ctypes.data_as(ctypes.c_void_p)) == 0
@@ -243,11 +247,19 @@ def test_pyramid_backing_default_and_opt_out(pkg, oracle, monkeypatch):
         _assert_same(ctx.pyramid(0), want, "one allocation")
 
 
-def test_default_variant_follows_geometry(pkg):
+def test_default_variant_follows_geometry(pkg, monkeypatch):
+    """default_variant (the one place the default is decided) from the width and the backing."""
     with pkg.PyramidContext(64, 4096, S=2, batch=2) as a, pkg.PyramidContext(64, 1920, S=2) as b, \
-            pkg.PyramidContext(4096, 4096, S=2, octaves=5) as c:
-        # 1920 wide: v11's 8 x 384 tile, in its flattened form v17 on the default chunked backing
-        assert a.tuning()["variant"] == 15 and b.tuning()["variant"] == 17 and c.tuning()["variant"] == 15
+            pkg.PyramidContext(4096, 4096, S=2, octaves=5) as c, pkg.PyramidContext(64, 640, S=2) as d:
+        # 1920 wide: the 8 x 384 tile, flattened (v17) on the default chunked backing; 640: 16 x 128
+        assert [x.tuning()["variant"] for x in (a, b, c, d)] == [15, 17, 15, 18]
+    monkeypatch.setenv("GDP_SPREAD_VMM", "0")
+    with pkg.PyramidContext(64, 1920, S=2) as b, pkg.PyramidContext(64, 4096, S=2) as a:
+        assert b.tuning()["variant"] == 11 and a.tuning()["variant"] == 15  # one hipMalloc: v11 for 1920
+    for v in (1, 19, 29, 30):  # removed in round 5 (never picked by an autotune)
+        with pkg.PyramidContext(64, 256, S=2) as x:
+            with pytest.raises(pkg.GdpError):
+                x.set_tuning(variant=v)
 
 
 def test_autotune_keeps_results_bit_exact(pkg, oracle):
@@ -255,7 +267,7 @@ def test_autotune_keeps_results_bit_exact(pkg, oracle):
     with pkg.PyramidContext(300, 512, S=2, octaves=5) as ctx:
         ctx.set_input(img)
         v, o, ms = ctx.autotune(iters=2)
-        assert 0 <= v <= 29 and o in (0, 1) and ms > 0
+        assert v in BUILD_VARIANTS and o in (0, 1) and ms > 0
         assert ctx.tuning()["variant"] == v and ctx.tuning()["tile_order"] == o
         ctx.build()
         _assert_same(ctx.pyramid(0), oracle.build_pyramid(img, 2, 5), ("autotuned", v, o))
@@ -1228,6 +1240,62 @@ def test_comm_exchange_halo_single_rank(pkg):
             assert [ctx.checksum(b) for b in range(2)] == before
         with pkg.PyramidContext(256, 256, S=2, octaves=5, batch=1, row_begin=0, row_end=128) as band:
             assert L.gdp_comm_exchange_halo(comm, band._ctx, None) != 0
+    finally:
+        L.gdp_comm_destroy(comm)
+
+
+@pytest.mark.gpu
+def test_comm_failure_closes_the_group_and_fails_fast(pkg):
+    """VERDICT r4 item 2 (the RCCL counterpart of the reference's per-row MPI_Send / MPI_Recv,
+    GaussDePyramid-MPI.h:285,298): a transfer that RCCL rejects INSIDE a group (test hook: a send
+    to peer `nranks`) makes the collective return an error with the group closed, marks the
+    communicator failed, and the next collective on it fails fast (GDP_ERR_STATE) instead of
+    hanging.  Group closed is shown by a fresh communicator on the same thread moving data: with
+    the group left open its transfers would be captured and never run (gdp_comm_check reads the
+    receive buffer back and compares)."""
+    import ctypes
+    import time
+
+    pkg.lib()
+    L = ctypes.CDLL(os.path.join(os.path.dirname(pkg.__file__), "lib", "libgdp_comm.so"))
+    L.gdp_comm_last_error.restype = ctypes.c_char_p
+
+    def new_comm():
+        uid = (ctypes.c_ubyte * 128)()
+        assert L.gdp_comm_unique_id(uid) == 0
+        comm = ctypes.c_void_p()
+        assert L.gdp_comm_init(ctypes.byref(comm), uid, 1, 0, 0) == 0, L.gdp_comm_last_error(None)
+        return comm
+
+    comm = new_comm()
+    try:
+        assert L.gdp_comm_check(comm, None) == 0, L.gdp_comm_last_error(comm)  # self send / recv moves data
+        assert L.gdp_comm_failed(comm) == 0
+        with pkg.PyramidContext(256, 256, S=2, octaves=5, batch=1) as ctx, \
+                pkg.PyramidContext(256, 256, S=2, octaves=5, batch=1) as full:
+            ctx.fill_synthetic(0x5EED, 0)
+            ctx.build()
+            ctx.sync()
+            want = ctx.checksum(0)
+            for call in (lambda: L.gdp_comm_exchange_halo(comm, ctx._ctx, None),
+                         lambda: L.gdp_comm_gather_bands(comm, ctx._ctx, 0, full._ctx, 0, 0, None),
+                         lambda: L.gdp_comm_check(comm, None)):
+                bad = comm
+                assert L.gdp_comm_test_inject_fault(bad) == 0
+                rc = call()
+                msg = L.gdp_comm_last_error(bad).decode()
+                assert rc == 2 and "group closed" in msg, (rc, msg)  # GDP_ERR_HIP
+                assert L.gdp_comm_failed(bad) == 1
+                t0 = time.perf_counter()
+                rc = call()
+                assert rc == 3 and "earlier collective" in L.gdp_comm_last_error(bad).decode(), rc  # GDP_ERR_STATE
+                assert time.perf_counter() - t0 < 1.0
+                L.gdp_comm_destroy(bad)  # aborts the failed communicator
+                comm = new_comm()
+                assert L.gdp_comm_check(comm, None) == 0, L.gdp_comm_last_error(comm)  # RCCL still runs here
+            # the same collective on the fresh communicator succeeds and leaves the build intact
+            assert L.gdp_comm_gather_bands(comm, ctx._ctx, 0, full._ctx, 0, 0, None) == 0, L.gdp_comm_last_error(comm)
+            assert full.checksum(0) == want
     finally:
         L.gdp_comm_destroy(comm)
 

@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "examples", "state_hip")
+EXE_MPITEST = os.path.join(REPO, "examples", "mpitest_hip")
 
 
 def _bits(a):
@@ -51,23 +52,24 @@ class _Replay:
             self.dirty = False
 
     def _push(self):
-        if self.mirror:
+        # mpitest.cpp's free functions always leave their result in the global GaussPy
+        if self.mirror or self.cls == "mpitest":
             self.host[:] = self.pyr
 
     def apply(self, op):
         f = op.split(":")
         n, S, O, o = self.n, self.S, self.O, self.o
-        intlen = "intlen" if self.cls in ("a512omp", "a512xp") else "serial"
+        intlen = "intlen" if self.cls in ("a512omp", "a512xp", "mpitest") else "serial"
         if f[0] == "init":
             self.pyr[:] = o.init_pyramid(self.img, S)
             self.dirty = False
             self._push()
-        elif f[0] in ("dog", "mpi", "nomp", "filter"):
+        elif f[0] in ("dog", "mpi", "omp", "nomp", "filter"):
             self._pull()
             if f[0] == "filter":
                 if self.cls != "a512omp":  # that class's GaussFilter is empty (:128-181)
                     o.gauss_octave(self.pyr, n, n, S, int(f[1]))
-            elif f[0] == "mpi":
+            elif f[0] in ("mpi", "omp"):
                 o.generate_dog(self.pyr, n, n, S, O, centre="intlen")
             elif f[0] == "nomp":
                 o.subset_a512omp(self.pyr, n, n, S, O)
@@ -163,6 +165,44 @@ def test_cpp_avx512_classes_process_host_edits(oracle, tmp_path):
         _run(oracle, tmp_path, "a512omp", n, 2, "lcg:11", ["neg:0:2", "dog", "filter:0", "set:1:4:1:1:-5", "dog"])
         _run(oracle, tmp_path, "a512xp", n, 2, "lcg:12", ["zero:1:1", "scale:0:0:1:-1", "dog", "neg:0:0", "filter:0",
                                                           "dog"])
+
+
+def _run_mpitest(oracle, tmp_path, n, S, spec, ops):
+    if not os.path.exists(EXE_MPITEST):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
+    out = tmp_path / "mpitest.f32"
+    subprocess.run([EXE_MPITEST, str(n), spec, str(out), "mpi", str(S), *ops], check=True, timeout=120,
+                   capture_output=True)
+    rp = _Replay(oracle, "mpitest", n, S, spec)
+    rp.apply("init")  # the driver's own GaussPyInit(p) before the ops
+    for op in ops:
+        rp.apply(op)
+    _assert_same(np.fromfile(out, dtype=np.float32), rp.host, ("mpitest", n, S, ops))
+
+
+@pytest.mark.parametrize("n,S", [(64, 2), (100, 2), (96, 3)])
+def test_cpp_mpitest_free_functions_process_host_edits(oracle, tmp_path, n, S):
+    """mpitest.cpp's GenerateDoG_mpi / _omp multiply and subtract the GLOBAL
+    GaussPy in place (mpitest.cpp:128-133, :165), so an edit written between GaussPyInit(p) and
+    GenerateDoG_mpi is processed.  The drop-in header (include/GaussDePyramid-HIP-mpitest.h) uploads
+    GaussPy before each call and runs the in-place pass: a zeroed level, scaled rows, negated
+    levels, values near FLT_MAX, re-seated rows -> bit-identical to the oracle's in-place
+    generate_dog with the integer-length centre on the same edited pyramid."""
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:31", EDITS + ["mpi"])
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:32", ["mpi"] + EDITS + ["omp", "neg:0:0", "mpi"])
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:33", EDITS + ["init", "mpi"])  # the refill overwrites the edits
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:34", ["reseat:0:1:3", "scale:0:1:3:-2", "omp", "reseat:1:0:0",
+                                                   "set:1:0:0:1:1e20", "mpi"])
+
+
+def test_cpp_mpitest_without_mirror_uploads_only_when_told(oracle, tmp_path):
+    """gdp_mpitest_mirror_host = false: edits reach the device only with host_dirty / SyncDevice;
+    the result is still left in GaussPy after every call (mpitest.cpp's callers read it)."""
+    n, S = 64, 2
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:35", ["mirror:0", "zero:0:1", "mpi"])  # edit never uploaded
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:35", ["mirror:0", "zero:0:1", "dirty", "mpi"])
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:35", ["mirror:0", "neg:0:2", "syncdev", "omp", "scale:0:0:5:3",
+                                                   "synchost", "mpi"])
 
 
 def test_python_mirror_processes_host_edits(pkg, oracle):
