@@ -207,57 +207,77 @@ def attach_cpu_baseline(result, args, rank, world, dist):
         dist.barrier()
 
 
+PMC_ARCHIVE = "pmc_records.json"  # the kept records of earlier rounds, one list (tools/prune_profiles.py)
+
+
+def pmc_records():
+    """Every PMC record under profiles/ as (name, record), in name order (later = newer): the
+    individual pmc_*.json files the collectors write, and the records gathered into
+    profiles/pmc_records.json (each keeps its original file name under "file").  A record's
+    citation is profiles/<file> when that file exists, else profiles/pmc_records.json#<file>."""
+    pdir = os.path.join(REPO, "profiles")
+    out = {}
+    if not os.path.isdir(pdir):
+        return []
+    names = sorted(f for f in os.listdir(pdir) if f.startswith("pmc_") and f.endswith(".json"))
+    stamp = tuple((f, os.path.getmtime(os.path.join(pdir, f))) for f in names)
+    if _PMC_CACHE.get("stamp") == stamp:
+        return _PMC_CACHE["records"]
+    agg = os.path.join(pdir, PMC_ARCHIVE)
+    if os.path.exists(agg):
+        with open(agg) as fh:
+            for rec in json.load(fh):
+                out[rec["file"]] = (f"{PMC_ARCHIVE}#{rec['file']}", {k: v for k, v in rec.items() if k != "file"})
+    for f in os.listdir(pdir):
+        if f.startswith("pmc_") and f.endswith(".json") and f != PMC_ARCHIVE:
+            try:
+                with open(os.path.join(pdir, f)) as fh:
+                    out[f] = (f, json.load(fh))
+            except (OSError, ValueError):
+                continue
+    _PMC_CACHE.update(stamp=stamp, records=[out[k] for k in sorted(out)])
+    return _PMC_CACHE["records"]
+
+
+_PMC_CACHE = {}
+
+
 def latest_conv_pmc(config_key, tun):
     """PMC record of the convolution extension's kernel on this workload with the run's conv
     kernel / rows / order (profiles/pmc_<cfg>_conv*_*.json), or None."""
-    pdir = os.path.join(REPO, "profiles")
     best = None
-    for f in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
-        if f.startswith("pmc_") and f.endswith(".json"):
-            try:
-                with open(os.path.join(pdir, f)) as fh:
-                    rec = json.load(fh)
-            except (OSError, ValueError):
-                continue
-            if rec.get("config") == config_key and rec.get("op") == "conv" and rec.get("kernel_bytes_per_launch") and \
-                    (rec.get("conv_kernel"), rec.get("conv_rows"), rec.get("conv_order")) == \
-                    (tun["conv_kernel"], tun["conv_rows"], tun["conv_order"]):
-                best = dict(rec, file=f)
+    for f, rec in pmc_records():
+        if rec.get("config") == config_key and rec.get("op") == "conv" and rec.get("kernel_bytes_per_launch") and \
+                (rec.get("conv_kernel"), rec.get("conv_rows"), rec.get("conv_order")) == \
+                (tun["conv_kernel"], tun["conv_rows"], tun["conv_order"]):
+            best = dict(rec, file=f)
     return best
 
 
 def latest_pmc(config_key, variant, tile_order, op="build", levels=5, zero_window=0, band_of=None,
                image_stride_mb=None, chunk_kb=None):
     """PMC-derived HBM bytes per launch of THIS kernel instance on this workload, from the newest
-    profiles/pmc_*.json (written by profiles/collect_pmc.py from separate rocprofv3 --pmc passes)
+    PMC record (pmc_records()) written by tools/pmc_variants.py from separate rocprofv3 --pmc passes,
     whose recorded build variant, tile order and zero-window mode equal the run's; None when no profile of that
     instance exists (the traffic of another variant would describe a different kernel).  band_of = N:
     the row-band config's per-rank launch at N ranks (rank 0's band of N, profiled on one GPU by
     tools/pmc_variants.py --band-of N), not the whole image's.  image_stride_mb: the spread layout's
-    records (GDP_IMAGE_STRIDE_MB), kept apart from the dense layout's.  chunk_kb: the run's pyramid
+    records (a GDP_EXPERIMENTS build), kept apart from the dense layout's.  chunk_kb: the run's pyramid
     backing (GDP_TUNE_PYRAMID_CHUNK_KB); a record of the same backing is preferred, else one of
     another backing (the backing moves pages, not bytes: DESIGN.md §4) — the file is named either way."""
-    pdir = os.path.join(REPO, "profiles")
     best, same = None, None
-    if os.path.isdir(pdir):
-        for f in sorted(os.listdir(pdir)):
-            if f.startswith("pmc_") and f.endswith(".json"):
-                try:
-                    with open(os.path.join(pdir, f)) as fh:
-                        rec = json.load(fh)
-                except (OSError, ValueError):
-                    continue
-                # the template instance too: k_build<5, ...> (S + 3 = 5 levels unrolled) or k_build<0, ...>
-                lt = f"k_build<{5 if levels == 5 else 0},"
-                if rec.get("config") == config_key and rec.get("op", "build") == op and \
-                        rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
-                        rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32" and \
-                        rec.get("zero_window", 0) == zero_window and rec.get("band_of") == band_of and \
-                        rec.get("image_stride_mb") == image_stride_mb and \
-                        lt in rec.get("kernel", lt):
-                    best = dict(rec, file=f)
-                    if rec.get("pyramid_chunk_kb", 0) == (chunk_kb or 0):
-                        same = best
+    # the template instance too: k_build<5, ...> (S + 3 = 5 levels unrolled) or k_build<0, ...>
+    lt = f"k_build<{5 if levels == 5 else 0},"
+    for f, rec in pmc_records():
+        if rec.get("config") == config_key and rec.get("op", "build") == op and \
+                rec.get("kernel_bytes_per_launch") and rec.get("variant") == variant and \
+                rec.get("tile_order") == tile_order and rec.get("input_format", "i32") == "i32" and \
+                rec.get("zero_window", 0) == zero_window and rec.get("band_of") == band_of and \
+                rec.get("image_stride_mb") == image_stride_mb and \
+                lt in rec.get("kernel", lt):
+            best = dict(rec, file=f)
+            if rec.get("pyramid_chunk_kb", 0) == (chunk_kb or 0):
+                same = best
     return same or best
 
 
@@ -266,18 +286,11 @@ def latest_inplace_pmc(config_key, op, tun):
     GDP_TUNE_INPLACE_SUB; --op gauss: k_window, keyed by GDP_TUNE_WINDOW_SUB) with the run's block
     shape, or None."""
     key = "inplace_sub" if op == "regen" else "window_sub"
-    pdir = os.path.join(REPO, "profiles")
     best = None
-    for f in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
-        if f.startswith("pmc_") and f.endswith(".json"):
-            try:
-                with open(os.path.join(pdir, f)) as fh:
-                    rec = json.load(fh)
-            except (OSError, ValueError):
-                continue
-            if rec.get("config") == config_key and rec.get("op") == op and rec.get("kernel_bytes_per_launch") and \
-                    rec.get(key) == tun[key] and rec.get("zero_window", 0) == tun.get("zero_window", 0):
-                best = dict(rec, file=f)
+    for f, rec in pmc_records():
+        if rec.get("config") == config_key and rec.get("op") == op and rec.get("kernel_bytes_per_launch") and \
+                rec.get(key) == tun[key] and rec.get("zero_window", 0) == tun.get("zero_window", 0):
+            best = dict(rec, file=f)
     return best
 
 
