@@ -12,10 +12,15 @@
 
 GaussPy is two-way state, as the reference's float**** is (:16; GaussFilter / GenerateDoG work
 on whatever the caller left in it, :122-131, :140-146): a level the caller touched through
-GaussPy[o][s] is a host array that may be written (g.GaussPy[o][s][r][c] = v, row slices,
-whole-level assignment), and every mutating call first uploads each such level back to the device
-(gdp_upload_level), so the edit is processed; GaussPyInit re-reads the CURRENT `data` (:80).
-Levels never touched cost nothing.  SyncDevice() uploads them on demand.
+GaussPy[o][s] is ONE host array for the object's lifetime (like a reference row, it stays live:
+a handle taken before a call reads the new contents after it, and writes through it are seen),
+and it may be written any way (g.GaussPy[o][s][r][c] = v, row slices, views, ufuncs with out=).
+Every mutating call first uploads each touched level whose bits differ from what the device last
+gave it (an exact comparison against a snapshot; levels only read are not uploaded, so reading
+GaussPy — output() included — never costs the fused GaussPyInit+GenerateDoG path), then runs,
+then refreshes every touched level in place.  GaussPyInit re-reads the CURRENT `data` (:80) and
+overwrites host edits, as the reference's refill does.  Levels never touched cost nothing.
+SyncDevice() uploads the edited levels on demand.
 
 Calling GenerateDoG() twice without GaussPyInit() re-filters the pyramid exactly like the
 reference's timing loop does (main.cpp:66-73).  The one behavioural difference is error
@@ -438,8 +443,10 @@ class GaussPyramid:
         self.S = int(S)
         self.layer = octaves_for(length)  # :48-53
         self._ctx = PyramidContext(length, length, self.S, self.layer, batch=1, device=device)
-        self._cache = {}
+        self._cache = {}  # (o, s) -> the level's host array (live for the object's lifetime)
+        self._snap = {}  # (o, s) -> the bits the device last gave that array (edit detection)
         self._fresh = False
+        self.uploaded_levels = 0  # levels the last SyncDevice uploaded (0: the host held no edits)
         self.GaussPyInit()  # :57
 
     # reference surface -------------------------------------------------------
@@ -449,14 +456,14 @@ class GaussPyramid:
         self._ctx.init()
         self.initialized = True
         self._fresh = True  # contents == init, so GenerateDoG may take the fused path
-        self._cache.clear()
+        self._refresh()  # every level refilled: host edits are overwritten, as in :76-86
 
     def GaussFilter(self, theLayer):
         """:106-134 — multiply every scale of octave `theLayer` by its window, in place."""
         self.SyncDevice()
         self._ctx.gauss_octave(int(theLayer))
         self._fresh = False
-        self._cache.clear()
+        self._refresh()
 
     def GenerateDoG(self):
         """:136-149 — GaussFilter + DoG for every octave, in place on the current contents."""
@@ -466,7 +473,7 @@ class GaussPyramid:
         else:
             self._ctx.generate_dog()
         self._fresh = False
-        self._cache.clear()
+        self._refresh()
 
     def output(self, file=None):
         """:89-104 — print scale 0 of each octave (space separated) and an `==` separator row."""
@@ -484,22 +491,40 @@ class GaussPyramid:
         return [_LevelView(self, o) for o in range(self.layer)]
 
     def SyncDevice(self):
-        """Upload every level the caller obtained through GaussPy (and so may have written) into the
-        device pyramid; the next call processes the host contents."""
-        if not self._cache:
-            return
-        for (o, s), arr in self._cache.items():
-            self._ctx.upload_level(0, o, s, arr)
-        self._cache.clear()
-        self._fresh = False  # the caller's contents, not necessarily GaussPyInit's
+        """Upload every level the caller obtained through GaussPy AND changed (its bits differ from
+        the device's last copy) into the device pyramid; the next call processes the host contents.
+        Sets `uploaded_levels`."""
+        n = 0
+        for key, arr in self._cache.items():
+            snap = self._snap[key]
+            if not np.array_equal(arr.view(np.uint32), snap.view(np.uint32)):
+                self._ctx.upload_level(0, key[0], key[1], arr)
+                snap[...] = arr
+                n += 1
+        self.uploaded_levels = n
+        if n:
+            self._fresh = False  # the caller's contents, not necessarily GaussPyInit's
 
     # helpers -----------------------------------------------------------------
     def _level(self, o, s):
         key = (o, s)
         if key not in self._cache:
             self._ctx.sync()
-            self._cache[key] = self._ctx.level(0, o, s)
+            arr = self._ctx.level(0, o, s)
+            self._cache[key] = arr
+            self._snap[key] = arr.copy()
         return self._cache[key]
+
+    def _refresh(self):
+        """After a device-side change: every touched level re-downloaded INTO its existing array,
+        so handles the caller holds stay live (the reference's rows never move)."""
+        if not self._cache:
+            return
+        self._ctx.sync()
+        for (o, s), arr in self._cache.items():
+            if arr.size:
+                check(lib().gdp_download_level(self._ctx._ctx, 0, int(o), int(s), _ptr(arr)), self._ctx._ctx)
+            self._snap[(o, s)][...] = arr
 
     def pyramid(self):
         """Packed [o][s][r][c] float32 copy (the oracle's layout)."""
@@ -534,7 +559,7 @@ class GaussPyramid_a512omp(GaussPyramid):
         if tiny < self.layer:
             self._ctx.dog_range(tiny, self.layer)  # ... and one for the repeat on sides <= 2
         self._fresh = False
-        self._cache.clear()
+        self._refresh()
 
     def GenerateDoG_nomp_dynamic(self):
         """:240-364 — scales 0..S-1 windowed, DoG for i < S-1: {DoG_0..DoG_{S-2}, G_{S-1}, x, x, x}."""
@@ -544,7 +569,7 @@ class GaussPyramid_a512omp(GaussPyramid):
         else:
             self._ctx.generate_dog_subset()
         self._fresh = False
-        self._cache.clear()
+        self._refresh()
 
     def GenerateDoG_nomp_static(self):
         """:366-368 — empty in the reference."""

@@ -237,6 +237,49 @@ def test_python_mirror_processes_host_edits(pkg, oracle):
     g.close()
 
 
+def test_python_mirror_handles_stay_live_and_reads_upload_nothing(pkg, oracle):
+    """a GaussPy[o][s] array taken before a call is the same live array after it (the
+    reference's rows never move): it reads the new contents, and writes through it — including
+    ones __setitem__ never sees (a row view, a ufunc with out=) — are processed by the next call.
+    Levels only read (output() included) are not uploaded, so GaussPyInit + reads + GenerateDoG
+    still takes the fused build; an unchanged pyramid uploads nothing."""
+    import io
+
+    n, S = 64, 2
+    O = oracle.octaves(n)
+    img = oracle.lcg_image(n, n, 41)
+    g = pkg.GaussPyramid(img, n, S)
+    lv = lambda p, o, s: oracle.levels(p, n, n, S, O)[(o, s)]  # noqa: E731
+    a = g.GaussPy[0][0]  # taken before any call
+    b = g.GaussPy[1][2]
+    g.output(file=io.StringIO())  # reads level (o, 0) of every octave
+    g.SyncDevice()
+    assert g.uploaded_levels == 0 and g._fresh  # reads uploaded nothing: GenerateDoG takes the fused build
+    g.GenerateDoG()
+    want = oracle.build_pyramid(img, S)
+    _assert_same(a, lv(want, 0, 0), "old handle reads the new level (0, 0)")
+    _assert_same(b, lv(want, 1, 2), "old handle reads the new level (1, 2)")
+    assert g.GaussPy[0][0] is a
+    row = a[3]
+    row *= np.float32(-2)  # through a view: no __setitem__ on `a`
+    np.multiply(b, np.float32(0.5), out=b)
+    lv(want, 0, 0)[3] *= np.float32(-2)
+    lv(want, 1, 2)[:] *= np.float32(0.5)
+    g.GenerateDoG()
+    assert g.uploaded_levels == 2
+    oracle.generate_dog(want, n, n, S, O)
+    _assert_same(g.pyramid(), want, "edits through old handles processed")
+    _assert_same(a, lv(want, 0, 0), "handle refreshed after the second call")
+    g.GenerateDoG()
+    assert g.uploaded_levels == 0  # the host mirror equals the device: nothing to upload
+    oracle.generate_dog(want, n, n, S, O)
+    _assert_same(g.pyramid(), want, "third call")
+    a[:] = 7.0  # edit, then GaussPyInit overwrites it (the refill, :76-86)
+    g.GaussPyInit()
+    _assert_same(a, lv(oracle.init_pyramid(img, S), 0, 0), "GaussPyInit refreshed the handle")
+    g.close()
+
+
 def test_inplace_zero_window_is_exact_for_caller_values_near_flt_max(pkg, oracle):
     """with S >= 3 some column taps exceed 1, so for a row outside the window support
     (fr = +0) v * fc can overflow to inf and inf * 0 = NaN — the zero-window shortcut of the
