@@ -675,13 +675,18 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     auto up = [gran](size_t v) { return (v + gran - 1) / gran * gran; };
     const char* ck = exp_env("GDP_SPREAD_CHUNK_MB");
     const char* ckk = exp_env("GDP_SPREAD_CHUNK_KB");
-    // Images stay dense (stride = one image's extent, as with one hipMalloc) unless an experiment
-    // spaces them (GDP_IMAGE_STRIDE_MB) or asks for one piece per image (GDP_SPREAD_CHUNK_MB=0):
-    // only then is the stride rounded to the allocation granularity.  The dense span itself is
-    // rounded up once, so a batch of small images costs at most one granule extra.
+    // Image starts: each image of the batch starts on an allocation granule (the layout every
+    // round-4 measurement of this backing ran with) only where that wastes at most 1/16 of an
+    // image — 1080x1920 (55 MB) and 4096^2 (447 MB) images; smaller images stay dense, so a batch
+    // of small images costs at most one granule extra (64x64 images were rounded from
+    // 27 KB to 2 MiB each).  GDP_IMAGE_ALIGN (GDP_EXPERIMENTS builds) forces 1 / 0 for A/B runs.
+    // An experiment that spaces the images (GDP_IMAGE_STRIDE_MB) or asks for one piece per image
+    // (GDP_SPREAD_CHUNK_MB=0) always aligns.
     const bool per_image = (ckk && std::atoll(ckk) <= 0) || (!ckk && ck && std::atoll(ck) <= 0);
     const size_t dense = (size_t)c->img_floats * 4;
-    const size_t img = per_image ? up(dense) : dense;
+    const char* al = exp_env("GDP_IMAGE_ALIGN");
+    const bool align_images = per_image || (al ? std::atoi(al) != 0 : (up(dense) - dense) * 16 <= dense);
+    const size_t img = align_images ? up(dense) : dense;
     const size_t stride = (size_t)g.pyr_stride * 4 > dense || per_image ? up(std::max((size_t)g.pyr_stride * 4, img)) : dense;
     g.pyr_stride = (long long)(stride / 4);
     const size_t span = up(stride * (size_t)g.batch);

@@ -190,10 +190,11 @@ def test_every_build_variant_is_bit_exact(pkg, oracle, variant):
 
 @pytest.mark.parametrize("H,W,B", [(300, 500, 3), (64, 64, 7), (1080, 1920, 2)])
 def test_chunked_backing_is_dense_and_bit_exact(pkg, oracle, monkeypatch, H, W, B):
-    """The default backing (2 MiB physical pieces in one reserved range) keeps the images DENSE:
-    gdp_pyramid_bytes is the batch's exact extent (no per-image rounding to the allocation
-    granularity), and every image, level, checksum and raw device-layout copy equals
-    the one-hipMalloc context's, in both tile orders."""
+    """The default backing (2 MiB physical pieces in one reserved range) rounds an image's
+    extent to the allocation granule only where that wastes at most 1/16 of it (small
+    images stay dense, gdp_pyramid_bytes is then the batch's exact extent), and every image,
+    level, checksum and raw device-layout copy equals the one-hipMalloc context's, in both tile
+    orders."""
     import ctypes
     imgs = [oracle.lcg_image(H, W, 40 + b) for b in range(B)]
     monkeypatch.setenv("GDP_SPREAD_VMM", "0")
@@ -212,7 +213,12 @@ def test_chunked_backing_is_dense_and_bit_exact(pkg, oracle, monkeypatch, H, W, 
     with pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) as ctx:
         assert ctx.tuning()["pyramid_chunk_kb"] > 0
         assert pkg.lib().gdp_image_floats(ctx._ctx) == n
-        assert pkg.lib().gdp_pyramid_bytes(ctx._ctx) == dense_bytes == n * B * 4
+        assert dense_bytes == n * B * 4
+        got_bytes = pkg.lib().gdp_pyramid_bytes(ctx._ctx)
+        if n * 4 < (32 << 20):  # a granule is > 1/16 of these images: dense
+            assert got_bytes == dense_bytes
+        else:
+            assert dense_bytes <= got_bytes <= dense_bytes * 17 // 16
         for b, im in enumerate(imgs):
             ctx.set_input(im, b)
         for order in (0, 1):
@@ -222,9 +228,14 @@ def test_chunked_backing_is_dense_and_bit_exact(pkg, oracle, monkeypatch, H, W, 
                 _assert_same(ctx.pyramid(b), oracle.build_pyramid(im, 2, 5), ("chunked", order, b))
                 assert ctx.checksum(b) == sums[b]
         got = np.empty(n, np.float32)
+        # the level extents of the raw device-layout image (the alignment padding between levels is
+        # never written: uninitialised in a hipMalloc, zero in fresh VMM pieces)
+        spans = [(ctx.level_offset(0, o, s), ctx.level_dims(o)[0] * ctx.level_dims(o)[1])
+                 for o in range(5) for s in range(5)]
         for b in range(B):
             assert pkg.lib().gdp_download_image_raw(ctx._ctx, b, got.ctypes.data_as(ctypes.c_void_p)) == 0
-            assert np.array_equal(got.view(np.uint32), raw[b].view(np.uint32))
+            for off, cnt in spans:
+                assert np.array_equal(got[off:off + cnt].view(np.uint32), raw[b][off:off + cnt].view(np.uint32))
         assert pkg.lib().gdp_upload_image_raw(ctx._ctx, 1, raw[0].ctypes.data_as(ctypes.c_void_p)) == 0
         assert ctx.checksum(1) == sums[0]
 

@@ -24,7 +24,9 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="4096x4096x1")
-    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=15)
+    ap.add_argument("--zero-window", type=int, default=1)
+    ap.add_argument("--store-pace", type=int, default=-1)
     ap.add_argument("--order", type=int, default=0)
     ap.add_argument("--rotate", type=int, default=5)
     args = ap.parse_args()
@@ -42,7 +44,8 @@ def main():
     ctxs = [pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) for _ in range(args.rotate)]
     for c in ctxs:
         c.fill_synthetic(0x5EED, 0)
-        c.set_tuning(variant=args.variant, tile_order=args.order)
+        c.set_tuning(variant=args.variant, tile_order=args.order, zero_window=args.zero_window,
+                     store_pace=args.store_pace)
     for _ in range(3):
         for c in ctxs:
             c.build()
@@ -59,7 +62,9 @@ def main():
         buf.zero_()
         torch.cuda.synchronize()
         assert lib.gdp_debug_set_block_trace(ctypes.c_void_p(buf.data_ptr())) == 0
-        ctxs[0].build()
+        ev_ms = ctypes.c_float()
+        # one traced launch between HIP events on the context's stream (gdp_time_builds, iters 1)
+        assert lib.gdp_time_builds(ctxs[0]._ctx, 1, None, ctypes.byref(ev_ms)) == 0
         ctxs[0].sync()
         assert lib.gdp_debug_set_block_trace(None) == 0
         t = buf.cpu().numpy().reshape(-1, 3)
@@ -87,6 +92,17 @@ def main():
         grid = np.linspace(0, span, 400)
         running = np.array([((start <= g) & (end > g)).sum() for g in grid])
         rec["us_below_half_resident"] = round(float((running < resident / 2).mean() * span), 2)
+        # ramp / drain split: the launch's HIP-event time vs the waves' span;
+        # ramp = first wave start -> running waves first reach 90 % of their peak; drain = running
+        # waves last at 90 % of the peak -> last wave's last store issued; after = event time not
+        # covered by any wave (dispatch before the first wave + completion after the last store)
+        peak = running.max()
+        hi = np.flatnonzero(running >= 0.9 * peak)
+        rec["event_us"] = round(ev_ms.value * 1e3, 2)
+        rec["ramp_us"] = round(float(grid[hi[0]]), 2)
+        rec["drain_us"] = round(span - float(grid[hi[-1]]), 2)
+        rec["steady_us"] = round(float(grid[hi[-1]] - grid[hi[0]]), 2)
+        rec["outside_waves_us"] = round(ev_ms.value * 1e3 - span, 2)
         rec["max_running_waves"] = int(running.max())
         rec["running_p50_over_span"] = int(np.median(running))
         # per CU (XCC, SE, SA?, CU from HW_ID) peak concurrency at the busiest sampled instant
