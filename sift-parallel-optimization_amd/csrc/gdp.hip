@@ -687,7 +687,8 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     const char* al = exp_env("GDP_IMAGE_ALIGN");
     const bool align_images = per_image || (al ? std::atoi(al) != 0 : (up(dense) - dense) * 16 <= dense);
     const size_t img = align_images ? up(dense) : dense;
-    const size_t stride = (size_t)g.pyr_stride * 4 > dense || per_image ? up(std::max((size_t)g.pyr_stride * 4, img)) : dense;
+    // an experiment's wider stride (GDP_IMAGE_STRIDE_MB set pyr_stride) is rounded to the granule
+    const size_t stride = (size_t)g.pyr_stride * 4 > dense ? up(std::max((size_t)g.pyr_stride * 4, img)) : img;
     g.pyr_stride = (long long)(stride / 4);
     const size_t span = up(stride * (size_t)g.batch);
     const char* ph = exp_env("GDP_SPREAD_PHYS_MB");
@@ -712,6 +713,13 @@ static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
         c->pyr_chunk_kb = -1;
     }
     const bool contiguous = stride == img;  // the pieces tile [0, span) with no unmapped gap
+    for (size_t k = 0; k < pieces.size(); ++k)  // host-side invariant: disjoint, granule-sized, in the span
+        if (pieces[k].second == 0 || pieces[k].first % gran || pieces[k].second % gran ||
+            pieces[k].first + pieces[k].second > span || (k && pieces[k].first < pieces[k - 1].first + pieces[k - 1].second)) {
+            where = "piece plan " + std::to_string(k) + " [" + std::to_string(pieces[k].first) + ", +" +
+                    std::to_string(pieces[k].second) + ") of span " + std::to_string(span);
+            return hipErrorInvalidValue;
+        }
     void* base = nullptr;
     where = "granularity " + std::to_string(gran) + ", span " + std::to_string(span) + ", pieces " +
             std::to_string(pieces.size()) + ": ";
