@@ -214,11 +214,9 @@ def test_chunked_backing_is_dense_and_bit_exact(pkg, oracle, monkeypatch, H, W, 
         assert ctx.tuning()["pyramid_chunk_kb"] > 0
         assert pkg.lib().gdp_image_floats(ctx._ctx) == n
         assert dense_bytes == n * B * 4
-        got_bytes = pkg.lib().gdp_pyramid_bytes(ctx._ctx)
-        if n * 4 < (32 << 20):  # a granule is > 1/16 of these images: dense
-            assert got_bytes == dense_bytes
-        else:
-            assert dense_bytes <= got_bytes <= dense_bytes * 17 // 16
+        # images start on an allocation granule (4 KiB on the MI355X boxes) only where that wastes
+        # at most 1/16 of an image
+        assert dense_bytes <= pkg.lib().gdp_pyramid_bytes(ctx._ctx) <= dense_bytes * 17 // 16
         for b, im in enumerate(imgs):
             ctx.set_input(im, b)
         for order in (0, 1):
@@ -312,7 +310,7 @@ def test_zero_window_path_is_bit_exact(pkg, oracle, zw):
                 ctx.set_tuning(zero_window=zw)
                 assert ctx.tuning()["zero_window"] == zw
                 ctx.set_input(img)
-                for v, sp in ((15, -1), (16, 0), (11, 1), (0, 3), (9, -1), (4, 0)):  # sp: GDP_TUNE_STORE_PACE
+                for v, sp in ((15, -1), (16, 0), (11, 1), (0, 3), (18, -1), (27, 0)):  # sp: GDP_TUNE_STORE_PACE
                     ctx.set_tuning(variant=v, store_pace=sp)
                     ctx.build()
                     _assert_same(ctx.pyramid(0), want, ("zero window", zw, H, W, S, O, centre, v, sp))

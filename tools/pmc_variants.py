@@ -45,11 +45,7 @@ def run(args):
         c.sync()
     order = []
     only = {int(x) for x in args.variants.split(",")} if args.variants else None
-    for v in range(64):
-        try:
-            ctxs[0].set_tuning(variant=v)
-        except pkg.GdpError:
-            break
+    for v in pkg.build_variants():
         if only is None or v in only:
             order += [(v, 0), (v, 1)]
     manifest = []

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv", "subset"],
                     help="default op; a variant may override it with op=... (e.g. 'v=15;v=15,op=subset')")
-    ap.add_argument("--variants", default="v=0;v=1;v=2;v=3;v=4;v=5;v=6;v=0,nt=0")
+    ap.add_argument("--variants", default="v=0;v=8;v=11;v=15;v=16;v=17;v=18;v=20;v=23;v=27;v=15,nt=0")
     ap.add_argument("--no-check", action="store_true", help="skip the same-output check (timing experiments)")
     ap.add_argument("--S", type=int, default=2, help="scales parameter S (S + 3 levels per octave)")
     ap.add_argument("--shape", default=None, help="HxWxBATCH overriding the config's shape (O stays 5)")
