@@ -103,6 +103,14 @@ def main():
         rec["drain_us"] = round(span - float(grid[hi[-1]]), 2)
         rec["steady_us"] = round(float(grid[hi[-1]] - grid[hi[0]]), 2)
         rec["outside_waves_us"] = round(ev_ms.value * 1e3 - span, 2)
+        # running waves over the launch in 20 equal bins (mean per bin), and per XCC the time its
+        # last wave issued its last store relative to the launch's last one
+        edges = np.linspace(0, span, 21)
+        rec["running_waves_20_bins"] = [int(running[(grid >= a) & (grid < b)].mean()) if ((grid >= a) & (grid < b)).any()
+                                        else 0 for a, b in zip(edges[:-1], edges[1:])]
+        ends = sorted(float(end[xcc == x].max()) for x in np.unique(xcc))
+        rec["xcc_end_spread_us"] = round(ends[-1] - ends[0], 2)
+        rec["xcc_end_mean_gap_us"] = round(ends[-1] - float(np.mean(ends)), 2)
         rec["max_running_waves"] = int(running.max())
         rec["running_p50_over_span"] = int(np.median(running))
         # per CU (XCC, SE, SA?, CU from HW_ID) peak concurrency at the busiest sampled instant
