@@ -248,8 +248,8 @@ def latest_conv_pmc(config_key, tun):
     best = None
     for f, rec in pmc_records():
         if rec.get("config") == config_key and rec.get("op") == "conv" and rec.get("kernel_bytes_per_launch") and \
-                (rec.get("conv_kernel"), rec.get("conv_rows"), rec.get("conv_order")) == \
-                (tun["conv_kernel"], tun["conv_rows"], tun["conv_order"]):
+                (rec.get("conv_kernel"), rec.get("conv_rows"), rec.get("conv_order"), rec.get("conv_halo", 2)) == \
+                (tun["conv_kernel"], tun["conv_rows"], tun["conv_order"], tun.get("conv_halo", 2)):
             best = dict(rec, file=f)
     return best
 
@@ -818,6 +818,8 @@ def main():
     ap.add_argument("--conv-order", type=int, default=None,
                     help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
                          "after their input rows; default 4)")
+    ap.add_argument("--conv-halo", type=int, default=None,
+                    help="--op conv: halo lanes per block-tile wave, 2 / 4 / 8 = 240 / 224 / 192-column tiles")
     ap.add_argument("--scatter", action="store_true",
                     help="N > 1: also measure the input split (rank 0's image batch, or for the row-band config its "
                          "image's rows, scattered over RCCL, SURVEY.md §8e), outside the timed region, and check the "
@@ -933,7 +935,8 @@ def main():
     if args.scatter and world > 1 and not halo_exchange:
         distribution = scatter_split(ctx, cfg, world, rank, dist, mg, backend, args.input)
     for c in ctxs:
-        c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order)
+        c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order,
+                     conv_halo=args.conv_halo)
         if args.op == "subset":  # that header's integer-length window centre (the same taps at these sizes)
             c.set_window_centre("intlen")
     autotuned = None
@@ -1112,8 +1115,9 @@ def main():
                         "gauss": "k_window (in-place row+column window, all octaves, %d-thread blocks), zero window %d%s"
                                  % (1024 // tun["window_sub"], tun["zero_window"], " (autotuned)" if autotuned else ""),
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
-                                 "240-column block tiles on %d waves, DPP lane shifts, store pace %s)"
-                                 % (ctx.tuning()["conv_rows"], ctx.tuning().get("conv_waves") or 16,
+                                 "%d-column block tiles on %d waves, DPP lane shifts, store pace %s)"
+                                 % (ctx.tuning()["conv_rows"], 4 * (64 - 2 * ctx.tuning()["conv_halo"]),
+                                    ctx.tuning().get("conv_waves") or 16,
                                     "off" if tun["conv_pace"] < 0 else "vmcnt(%d)" % tun["conv_pace"])
                                  if ctx.tuning()["conv_kernel"] == 2 and S <= 5 else
                                  "k_conv_sweep (extension: separable Gaussian convolution, register sweep + "
@@ -1134,6 +1138,9 @@ def main():
         result["autotune"] = {"seconds": round(tune_s, 2), "candidates": (
             len(pkg.build_variants()) * (8 if args.op == "build" else 6) if args.op in ("build", "subset")
             else None), "rounds": 5}
+    result["tuning"] = {k: tun[k] for k in ("variant", "tile_order", "zero_window", "store_pace", "inplace_sub",
+                                            "window_sub", "inplace_pace", "conv_kernel", "conv_rows", "conv_order",
+                                            "conv_waves", "conv_halo", "conv_pace", "pyramid_chunk_kb") if k in tun}
     result["topology"] = topology
     if distribution is not None:
         result["distribution"] = distribution

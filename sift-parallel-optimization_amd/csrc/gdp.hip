@@ -435,7 +435,9 @@ static void conv_sweep_geom(gdp_ctx* c) {
         const long long rows_per_blk = (long long)kSwWaves * conv_sweep_rows(c);
         g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
         const long long bk_rows = c->conv_rows;
-        g.bk_blk[o + 1] = g.bk_blk[o] + (sweep ? (unsigned)((og.rows + bk_rows - 1) / bk_rows * g.sw_strips_c[o]) : 0u);
+        const int bk_cols = 4 * (64 - 2 * g.bk_halo_lanes);  // block-tile output columns (240 / 224 / 192)
+        g.bk_strips_c[o] = (og.cols + bk_cols - 1) / bk_cols;
+        g.bk_blk[o + 1] = g.bk_blk[o] + (sweep ? (unsigned)((og.rows + bk_rows - 1) / bk_rows * g.bk_strips_c[o]) : 0u);
         g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
     }
     c->conv_perm_dirty = true;
@@ -461,20 +463,20 @@ static int conv_follow_rows(gdp_ctx* c) { return c->conv_rows_set ? GDP_OK : con
 // issued right after the octave-0 block row that covers the last of its input rows, so the
 // decimated rows it reads were just brought on chip by octave 0 instead of being fetched again.
 // `blk` is the block prefix of the kernel that will run (sw_blk or bk_blk).
-static int conv_sweep_perm(gdp_ctx* c, const unsigned* blk) {
+static int conv_sweep_perm(gdp_ctx* c, const unsigned* blk, const int* strips) {
     const Geom& g = c->geom;
     std::vector<unsigned> perm;
     perm.reserve(blk[g.O]);
     auto emit_row = [&](int o, unsigned tr) {
-        const unsigned sc = (unsigned)g.sw_strips_c[o];
+        const unsigned sc = (unsigned)strips[o];
         for (unsigned tc = 0; tc < sc; ++tc) perm.push_back(blk[o] + tr * sc + tc);
     };
-    const unsigned rows0 = g.oct[0].cols ? (blk[1] - blk[0]) / std::max(1u, (unsigned)g.sw_strips_c[0]) : 0;
+    const unsigned rows0 = g.oct[0].cols ? (blk[1] - blk[0]) / std::max(1u, (unsigned)strips[0]) : 0;
     std::vector<unsigned> next(g.O, 0); // next block row of each octave
     for (unsigned k = 0; k < rows0; ++k) {
         emit_row(0, k);
         for (int o = 1; o < g.O; ++o) {
-            const unsigned sc = (unsigned)std::max(1, g.sw_strips_c[o]);
+            const unsigned sc = (unsigned)std::max(1, strips[o]);
             const unsigned nrows = (blk[o + 1] - blk[o]) / sc;
             // octave-o block row tr covers octave-0 block rows [2^o tr, 2^o (tr + 1))
             while (next[o] < nrows && ((unsigned long long)(next[o] + 1) << o) <= (unsigned long long)k + 1)
@@ -482,7 +484,7 @@ static int conv_sweep_perm(gdp_ctx* c, const unsigned* blk) {
         }
     }
     for (int o = 1; o < g.O; ++o) { // leftovers (octave 0 swept nothing, or rounding at the bottom)
-        const unsigned sc = (unsigned)std::max(1, g.sw_strips_c[o]);
+        const unsigned sc = (unsigned)std::max(1, strips[o]);
         const unsigned nrows = (blk[o + 1] - blk[o]) / sc;
         while (next[o] < nrows) emit_row(o, next[o]++);
     }
@@ -506,9 +508,9 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int L, int T, int W>
+template <int L, int T, int W, int HL = 2>
 hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
-    auto k = k_conv_blk<L, T, W>;
+    auto k = k_conv_blk<L, T, W, HL>;
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
                        c->d_conv_perm);
@@ -522,6 +524,7 @@ template <int L>
 hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
     const int T = c->conv_rows, W = c->conv_waves;
     if (W == 8) {
+        if (c->geom.bk_halo_lanes != 2) return hipErrorInvalidConfiguration;  // 8 waves: 240-column tiles only
         switch (T) {
             case 8: return launch_conv_blk_t<L, 8, 8>(c, units, st);
             case 16: return launch_conv_blk_t<L, 16, 8>(c, units, st);
@@ -531,10 +534,17 @@ hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
         }
     }
     if (W != 16) return hipErrorInvalidConfiguration;
-    switch (T) {
-        case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
-        case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
-        case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
+    // 16 waves: halo lanes 2 (240-column tiles), 4 (224) or 8 (192, line-aligned loads and stores)
+    switch (T * 16 + c->geom.bk_halo_lanes) {
+        case 16 * 16 + 2: return launch_conv_blk_t<L, 16, 16, 2>(c, units, st);
+        case 32 * 16 + 2: return launch_conv_blk_t<L, 32, 16, 2>(c, units, st);
+        case 48 * 16 + 2: return launch_conv_blk_t<L, 48, 16, 2>(c, units, st);
+        case 16 * 16 + 4: return launch_conv_blk_t<L, 16, 16, 4>(c, units, st);
+        case 32 * 16 + 4: return launch_conv_blk_t<L, 32, 16, 4>(c, units, st);
+        case 48 * 16 + 4: return launch_conv_blk_t<L, 48, 16, 4>(c, units, st);
+        case 16 * 16 + 8: return launch_conv_blk_t<L, 16, 16, 8>(c, units, st);
+        case 32 * 16 + 8: return launch_conv_blk_t<L, 32, 16, 8>(c, units, st);
+        case 48 * 16 + 8: return launch_conv_blk_t<L, 48, 16, 8>(c, units, st);
         default: return hipErrorInvalidConfiguration;
     }
 }
@@ -868,6 +878,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // the convolution block tiles' five stores per output row go out back to back; vmcnt(2) after
     // each measured 0.5-1.3 % faster on 4096^2 / 64 x 4096^2 / 16384^2 (profiles/sp_conv_c*_r03ap.log)
     g.conv_pace = 2;
+    g.bk_halo_lanes = 2;
     c->in_pitch_own = g.in_pitch;
     c->in_img_stride_own = g.in_img_stride;
 
@@ -1378,7 +1389,7 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     }
     const unsigned* blk = c->conv_kernel == 2 ? g.bk_blk : g.sw_blk;
     if (sweep && (c->conv_order & 4) && (c->conv_perm_dirty || c->conv_perm_kernel != c->conv_kernel)) {
-        const int rc = conv_sweep_perm(c, blk);
+        const int rc = conv_sweep_perm(c, blk, c->conv_kernel == 2 ? g.bk_strips_c : g.sw_strips_c);
         if (rc != GDP_OK) return rc;
         c->conv_perm_kernel = c->conv_kernel;
     }
@@ -1976,6 +1987,7 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_STORE_PACE: *value = c->geom.store_pace; return GDP_OK;
         case GDP_TUNE_INPLACE_PACE: *value = c->geom.inplace_pace; return GDP_OK;
         case GDP_TUNE_CONV_PACE: *value = c->geom.conv_pace; return GDP_OK;
+        case GDP_TUNE_CONV_HALO: *value = c->geom.bk_halo_lanes; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -2022,6 +2034,8 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
         }
         case GDP_TUNE_CONV_WAVES:
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
+            if (value == 8 && c->geom.bk_halo_lanes != 2)
+                return c->status(GDP_ERR_ARG, "8-wave block tiles take halo lanes 2 only (GDP_TUNE_CONV_HALO)");
             c->conv_waves = value;
             return conv_follow_rows(c);
         case GDP_TUNE_STORE_PACE:
@@ -2052,6 +2066,21 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;
             return GDP_OK;
+        case GDP_TUNE_CONV_HALO: {
+            if (value != 2 && value != 4 && value != 8)
+                return c->status(GDP_ERR_ARG, "conv halo lanes must be 2 (240-column block tiles), 4 (224) or 8 (192)");
+            if (value != 2 && c->conv_waves != 16)
+                return c->status(GDP_ERR_ARG, "conv halo lanes 4 / 8 need 16-wave block tiles");
+            const int old = c->geom.bk_halo_lanes;
+            c->geom.bk_halo_lanes = value;
+            conv_sweep_geom(c);
+            const int rc = upload_geom(c);
+            if (rc != GDP_OK) {
+                c->geom.bk_halo_lanes = old;
+                conv_sweep_geom(c);
+            }
+            return rc;
+        }
         case GDP_TUNE_BUILD_LDS:
             if (value < 0 || value > 160 * 1024) return c->status(GDP_ERR_ARG, "build LDS bytes must be in [0, 163840]");
             c->build_lds = value;
