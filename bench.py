@@ -203,6 +203,8 @@ def attach_cpu_baseline(result, args, rank, world, dist):
             base["when"] = (f"rank 0, after all {world} ranks finished their timed steps; ranks 1..{world - 1} "
                             f"waited at a barrier meanwhile (no GPU work during the sample)")
         result["cpu_baseline"] = base
+        if args.op == "build" and world == 1:
+            result["dropin_call"] = dropin_call_cost()
     if dist is not None and world > 1:
         dist.barrier()
 
@@ -240,6 +242,37 @@ def pmc_records():
 
 
 _PMC_CACHE = {}
+
+
+def dropin_call_cost(n=4096, calls=5):
+    """Per-call cost of the C++ drop-in class (include/GaussDePyramid-HIP.h, main.cpp's timing loop:
+    GenerateDoG() on the same object) through examples/state_hip, outside the timed region: with
+    the default two-way GaussPy (mirror_host: upload + in-place pass + download of the whole
+    pyramid over PCIe every call, pipelined over row chunks) and with mirror_host = false (the
+    device pyramid is the state; no PCIe).  ADVICE r4: the mirror's cost, measured."""
+    import re
+    import subprocess
+
+    exe = os.path.join(REPO, "examples", "state_hip")
+    if not os.path.exists(exe):
+        return None
+    out = {"n": n, "S": 2, "calls": calls, "source": "examples/state_hip hip <n> 2 ones - [mirror:0] time:<calls>"}
+    for key, ops in (("mirror_host_ms", []), ("device_state_ms", ["mirror:0"])):
+        r = subprocess.run([exe, "hip", str(n), "2", "ones", "-", *ops, f"time:{calls}"], capture_output=True, text=True,
+                           timeout=120)
+        m = re.search(r"([0-9.]+) ms per GenerateDoG", r.stderr)
+        out[key] = float(m.group(1)) if (r.returncode == 0 and m) else None
+    if out.get("mirror_host_ms"):
+        pyr = 4 * 5 * pyramid_pixels(n, n, octaves_for(n))  # bytes each way per call
+        out["pcie_GBps_each_way"] = round(pyr / (out["mirror_host_ms"] / 1e3) / 1e9, 1)
+    return out
+
+
+def octaves_for(n):
+    x = 0
+    while n > 0:
+        x, n = x + 1, n // 2
+    return x
 
 
 def latest_conv_pmc(config_key, tun):

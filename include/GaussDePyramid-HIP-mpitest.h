@@ -130,12 +130,18 @@ static inline void gdp_mpitest_generate() {
     auto begin = std::chrono::steady_clock::now();
     // the GLOBAL GaussPy is what the reference's workers multiply and its collector subtracts
     // (:128-133, :165): upload it first, then the in-place pass on exactly those contents
-    if (gdp_mpitest_mirror_host || gdp_mpitest_host_dirty) gdp_mpitest_SyncDevice();
-    gdp_mpitest_check(gdp_mpitest_fresh ? gdp_build(gdp_mpitest_ctx, nullptr) : gdp_generate_dog(gdp_mpitest_ctx, nullptr),
-                      "GenerateDoG_mpi");
-    gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");
+    if (gdp_mpitest_mirror_host && gdp_mpitest_rows_in_mirror()) {
+        // upload + in-place pass + download in one call, pipelined over row chunks
+        gdp_mpitest_check(gdp_generate_dog_mirrored(gdp_mpitest_ctx, 0, gdp_mpitest_host), "GenerateDoG_mpi");
+        gdp_mpitest_host_dirty = false;
+    } else {
+        if (gdp_mpitest_mirror_host || gdp_mpitest_host_dirty) gdp_mpitest_SyncDevice();
+        gdp_mpitest_check(gdp_mpitest_fresh ? gdp_build(gdp_mpitest_ctx, nullptr) : gdp_generate_dog(gdp_mpitest_ctx, nullptr),
+                          "GenerateDoG_mpi");
+        gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");
+        gdp_mpitest_check(gdp_mpitest_download(), "GenerateDoG_mpi");
+    }
     gdp_mpitest_fresh = false;
-    gdp_mpitest_check(gdp_mpitest_download(), "GenerateDoG_mpi");
     auto end = std::chrono::steady_clock::now();
     std::cout << std::chrono::duration<double>(end - begin).count() << std::endl;
 }

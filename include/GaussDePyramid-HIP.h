@@ -24,7 +24,9 @@
 //    GenerateDoG_mpi) the host GaussPy is uploaded to the device, and after it the device pyramid
 //    is copied back into GaussPy; GaussPyInit re-reads `data` (:80).  A caller may write
 //    g.GaussPy[o][s][r][c] (or g.data[r][c]) at any time and the next call processes the edit.
-//    Cost: one pyramid H2D + one D2H per call (PCIe; 447 MB each way at 4096^2).
+//    Cost: one pyramid H2D + one D2H per call (PCIe; 447 MB each way at 4096^2);
+//    GenerateDoG / GenerateDoG_mpi overlap the two directions and the kernel over row chunks
+//    (gdp_generate_dog_mirrored) while the rows still point into the pinned mirror.
 //  - mirror_host = false: the device pyramid is the state; GaussPy is refreshed only by
 //    SyncHost(), and host edits reach the device only through SyncDevice() — or set
 //    `host_dirty = true` after editing and the next mutating call uploads first (then clears it).
@@ -176,6 +178,14 @@ inline void GaussPyramid_hip::GaussFilter(int theLayer) {
 }
 
 inline void GaussPyramid_hip::GenerateDoG() {
+    if (mirror_host && rows_in_mirror_()) {
+        // GaussPy mirrored in the pinned device-layout buffer: upload, in-place pass and download
+        // in one call, pipelined over row chunks (both PCIe directions and the kernel overlap)
+        check_(ctx_, gdp_generate_dog_mirrored(ctx_, 0, host_), "GenerateDoG");
+        host_dirty = false;
+        fresh_ = false;
+        return;
+    }
     // on freshly initialised contents the fused single-pass build is bit-identical to
     // GaussFilter + DoG in place; otherwise run the in-place pass on what is there
     pull_host_();
@@ -188,8 +198,17 @@ inline void GaussPyramid_hip::GenerateDoG() {
 inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
     // switching centres selects the other device tap table (no drain, no re-upload after the
     // first call); both calls below are ordered on the context's stream
-    pull_host_();
+    const bool piped = mirror_host && rows_in_mirror_();  // see GenerateDoG
+    if (!piped) pull_host_();
     check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi");
+    if (piped) {
+        const int rc = gdp_generate_dog_mirrored(ctx_, 0, host_);
+        check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi");
+        check_(ctx_, rc, "GenerateDoG_mpi");
+        host_dirty = false;
+        fresh_ = false;
+        return;
+    }
     const int rc = fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr);
     check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi");
     check_(ctx_, rc, "GenerateDoG_mpi");

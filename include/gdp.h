@@ -253,6 +253,14 @@ int gdp_host_alloc(size_t bytes, void** host);
 void gdp_host_free(void* host);
 size_t gdp_image_floats(const gdp_ctx* ctx);
 int gdp_download_image_raw(gdp_ctx* ctx, int b, float* host);
+/* GenerateDoG (in place, all octaves, the context's window centre) of image `b` held in HOST
+ * memory in the raw device layout (gdp_download_image_raw's format, `gdp_image_floats` floats):
+ * bit-identical to gdp_upload_image_raw(b, host) + gdp_generate_dog + gdp_download_image_raw(b,
+ * host) for that image, but pipelined over row chunks so the host-to-device copies, the kernel and
+ * the device-to-host copies overlap (two copy streams beside the context's).  `host` should be
+ * pinned (gdp_host_alloc) for the copies to be asynchronous.  Blocking.  This is what the C++
+ * drop-ins run for GenerateDoG() when GaussPy is mirrored (mirror_host, the default). */
+int gdp_generate_dog_mirrored(gdp_ctx* ctx, int b, float* host);
 /* Order-independent 64-bit checksum of image b's pyramid (blocking): the sum, mod 2^64, over
  * every word of every level of splitmix64_fin(idx * 0x9E3779B97F4A7C15 + (o*64+s) *
  * 0xD1B54A32D192ED03 + float_bits), idx = global_row * cols + col.  Row-band checksums add up

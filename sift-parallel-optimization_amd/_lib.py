@@ -99,6 +99,7 @@ SIGNATURES = {
     "gdp_host_free": (None, [_p]),
     "gdp_image_floats": (_c_size, [_p]),
     "gdp_download_image_raw": (_c_int, [_p, _c_int, _p]),
+    "gdp_generate_dog_mirrored": (_c_int, [_p, _c_int, _p]),
     "gdp_checksum": (_c_int, [_p, _c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "gdp_get_taps": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_set_window_centre": (_c_int, [_p, _c_int]),

@@ -146,6 +146,9 @@ struct gdp_ctx {
                                   // pyramid download 8.77 vs 9.99 ms with 4, tools/mirror_bench.py; capped by
                                   // the host's hardware threads at context creation)
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
+    // gdp_generate_dog_mirrored: copy streams (host -> device, device -> host) and per-chunk events
+    hipStream_t st_up = nullptr, st_down = nullptr;
+    std::vector<hipEvent_t> ev_mirror;
     unsigned long long* d_sum = nullptr;
     std::vector<float> h_taps;
     long long in_pitch_own = 0, in_img_stride_own = 0;
@@ -1071,6 +1074,10 @@ void gdp_destroy(gdp_ctx* c) {
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->ev_stage)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_mirror)
+        if (e) (void)hipEventDestroy(e);
+    if (c->st_up) (void)hipStreamDestroy(c->st_up);
+    if (c->st_down) (void)hipStreamDestroy(c->st_down);
     if (c->d_sum) (void)hipFree(c->d_sum);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1838,6 +1845,73 @@ int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
     GDP_HIP(c, hipSetDevice(c->device));
     GDP_HIP(c, hipMemcpyAsync(host, c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->img_floats * 4,
                               hipMemcpyDeviceToHost, c->stream));
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+// GenerateDoG on a HOST pyramid (the drop-in classes' mirrored GaussPy, GuassDePyramid.h:16,
+// :136-149): = gdp_upload_image_raw(b, host) + the in-place GenerateDoG of image b +
+// gdp_download_image_raw(b, host), bit for bit, but pipelined over row chunks so the PCIe copies in
+// both directions and the kernel overlap: chunk j's upload (copy stream 1) runs beside chunk j-1's
+// pass (the context's stream) and chunk j-2's download (copy stream 2).  The op is pointwise in
+// (octave, row, column) across the S+3 levels, so any row split is exact.
+int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored: bad argument") : GDP_ERR_ARG;
+    const Geom& g = c->geom;
+    GDP_HIP(c, hipSetDevice(c->device));
+    if (!c->st_up) GDP_HIP(c, hipStreamCreateWithFlags(&c->st_up, hipStreamNonBlocking));
+    if (!c->st_down) GDP_HIP(c, hipStreamCreateWithFlags(&c->st_down, hipStreamNonBlocking));
+    // chunks of about 1/16 of the image's bytes: octave 0 in ~12 row ranges, each smaller octave in
+    // proportionally fewer (one for the tiny ones)
+    struct Chunk { int o, r0, r1; };
+    std::vector<Chunk> chunks;
+    long long total = 0;
+    for (int o = 0; o < g.O; ++o) total += (long long)g.oct[o].rows * g.oct[o].cols;
+    const long long target = std::max(1ll, total / 16);
+    for (int o = 0; o < g.O; ++o) {
+        const OctGeom& og = g.oct[o];
+        if ((long long)og.rows * og.cols == 0) continue;
+        const long long px = (long long)og.rows * og.cols;
+        const int n = (int)std::max(1ll, std::min<long long>(og.rows, (px + target / 2) / target));
+        for (int k = 0; k < n; ++k) {
+            const int r0 = (int)((long long)og.rows * k / n), r1 = (int)((long long)og.rows * (k + 1) / n);
+            if (r1 > r0) chunks.push_back({o, r0, r1});
+        }
+    }
+    const size_t need = 2 * chunks.size() + 1;
+    while (c->ev_mirror.size() < need) {
+        hipEvent_t e;
+        GDP_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->ev_mirror.push_back(e);
+    }
+    hipEvent_t* ev = c->ev_mirror.data();
+    // the uploads overwrite levels earlier work on the context's stream may still use
+    GDP_HIP(c, hipEventRecord(ev[2 * chunks.size()], c->stream));
+    GDP_HIP(c, hipStreamWaitEvent(c->st_up, ev[2 * chunks.size()], 0));
+    auto image_level = [&](int o, int s) { return g.oct[o].lev_off + (long long)s * g.oct[o].lev_stride; };
+    for (size_t j = 0; j < chunks.size(); ++j) {
+        const Chunk& ch = chunks[j];
+        const OctGeom& og = g.oct[ch.o];
+        const size_t off = (size_t)ch.r0 * og.cols, n = (size_t)(ch.r1 - ch.r0) * og.cols;
+        for (int s = 0; s < g.L; ++s)
+            GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, ch.o, s)) + off,
+                                      host + image_level(ch.o, s) + off, n * 4, hipMemcpyHostToDevice, c->st_up));
+        GDP_HIP(c, hipEventRecord(ev[2 * j], c->st_up));
+        GDP_HIP(c, hipStreamWaitEvent(c->stream, ev[2 * j], 0));
+        const unsigned k0 = (unsigned)ch.r0 * (unsigned)og.gpr, k1 = (unsigned)ch.r1 * (unsigned)og.gpr;
+        auto kern = c->nontemporal ? k_levels_range<0, 3, true> : k_levels_range<0, 3, false>;
+        if (g.L == 5) kern = c->nontemporal ? k_levels_range<5, 3, true> : k_levels_range<5, 3, false>;
+        hipLaunchKernelGGL(kern, dim3((k1 - k0 + 255) / 256), dim3(256), 0, c->stream, c->d_geom, c->d_out, c->d_taps,
+                           (unsigned)b, ch.o, k0, k1);
+        GDP_HIP(c, hipGetLastError());
+        GDP_HIP(c, hipEventRecord(ev[2 * j + 1], c->stream));
+        GDP_HIP(c, hipStreamWaitEvent(c->st_down, ev[2 * j + 1], 0));
+        for (int s = 0; s < g.L; ++s)
+            GDP_HIP(c, hipMemcpyAsync(host + image_level(ch.o, s) + off, gdp_device_level(c, b, ch.o, s) + off, n * 4,
+                                      hipMemcpyDeviceToHost, c->st_down));
+    }
+    GDP_HIP(c, hipStreamSynchronize(c->st_down));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
 } GDP_ABI_CATCH(c)

@@ -280,6 +280,65 @@ def test_python_mirror_handles_stay_live_and_reads_upload_nothing(pkg, oracle):
     g.close()
 
 
+@pytest.mark.parametrize("H,W,S,B,centre,zw", [(4096, 4096, 2, 1, "serial", 1), (300, 500, 3, 2, "intlen", 0),
+                                                (1080, 1920, 2, 2, "serial", 1), (7, 5, 0, 1, "serial", 0)])
+def test_generate_dog_mirrored_equals_upload_pass_download(pkg, oracle, H, W, S, B, centre, zw):
+    """gdp_generate_dog_mirrored (the drop-ins' GenerateDoG on a mirrored GaussPy: upload, in-place
+    pass and download pipelined over row chunks on three streams) == gdp_upload_image_raw +
+    gdp_generate_dog + gdp_download_image_raw, bit for bit, on an edited pyramid (values up to 3e38,
+    negatives, zeros), for the image it names only; the other images of the batch are untouched."""
+    import ctypes
+
+    L = pkg.lib()
+    rng = np.random.default_rng(H + W + S)
+    with pkg.PyramidContext(H, W, S=S, batch=B) as a, pkg.PyramidContext(H, W, S=S, batch=B) as m:
+        n = L.gdp_image_floats(a._ctx)
+        raw = []
+        for b in range(B):
+            img = oracle.lcg_image(H, W, 50 + b)
+            for c in (a, m):
+                c.set_window_centre(centre)
+                c.set_tuning(zero_window=zw)
+                c.set_input(img, b)
+        for c in (a, m):
+            c.build()
+            c.sync()
+        for b in range(B):
+            r = np.empty(n, np.float32)
+            assert L.gdp_download_image_raw(a._ctx, b, r.ctypes.data_as(ctypes.c_void_p)) == 0
+            r[rng.integers(0, n, 64)] = np.float32(3e38)
+            r[rng.integers(0, n, 64)] *= np.float32(-7.5)
+            r[rng.integers(0, n, 64)] = 0.0
+            raw.append(r)
+            for c in (a, m):
+                assert L.gdp_upload_image_raw(c._ctx, b, r.ctypes.data_as(ctypes.c_void_p)) == 0
+        tgt = B - 1
+        a.generate_dog()  # every image of the batch; only image tgt is compared
+        a.sync()
+        want = np.empty(n, np.float32)
+        assert L.gdp_download_image_raw(a._ctx, tgt, want.ctypes.data_as(ctypes.c_void_p)) == 0
+        hptr = ctypes.c_void_p()
+        assert L.gdp_host_alloc(n * 4, ctypes.byref(hptr)) == 0
+        try:
+            host = np.ctypeslib.as_array(ctypes.cast(hptr, ctypes.POINTER(ctypes.c_float)), shape=(n,))
+            host[:] = raw[tgt]
+            assert L.gdp_generate_dog_mirrored(m._ctx, tgt, hptr) == 0
+            spans = [(m.level_offset(0, o, s), m.level_dims(o)[0] * m.level_dims(o)[1])
+                     for o in range(m.O) for s in range(S + 3)]
+            for off, cnt in spans:  # the level extents (the padding between levels is never written)
+                _assert_same_nan(host[off:off + cnt], want[off:off + cnt], ("host", H, W, off))
+            got = np.empty(n, np.float32)
+            assert L.gdp_download_image_raw(m._ctx, tgt, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            for off, cnt in spans:
+                _assert_same_nan(got[off:off + cnt], want[off:off + cnt], ("device", H, W, off))
+            for b in range(B - 1):  # untouched
+                assert L.gdp_download_image_raw(m._ctx, b, got.ctypes.data_as(ctypes.c_void_p)) == 0
+                for off, cnt in spans:
+                    _assert_same_nan(got[off:off + cnt], raw[b][off:off + cnt], ("other image", b))
+        finally:
+            L.gdp_host_free(hptr)
+
+
 def test_inplace_zero_window_is_exact_for_caller_values_near_flt_max(pkg, oracle):
     """with S >= 3 some column taps exceed 1, so for a row outside the window support
     (fr = +0) v * fc can overflow to inf and inf * 0 = NaN — the zero-window shortcut of the
