@@ -851,8 +851,6 @@ def main():
     ap.add_argument("--conv-order", type=int, default=None,
                     help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
                          "after their input rows; default 4)")
-    ap.add_argument("--conv-halo", type=int, default=None,
-                    help="--op conv: halo lanes per block-tile wave, 2 / 4 / 8 = 240 / 224 / 192-column tiles")
     ap.add_argument("--scatter", action="store_true",
                     help="N > 1: also measure the input split (rank 0's image batch, or for the row-band config its "
                          "image's rows, scattered over RCCL, SURVEY.md §8e), outside the timed region, and check the "
@@ -969,7 +967,7 @@ def main():
         distribution = scatter_split(ctx, cfg, world, rank, dist, mg, backend, args.input)
     for c in ctxs:
         c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order,
-                     conv_halo=args.conv_halo)
+)
         if args.op == "subset":  # that header's integer-length window centre (the same taps at these sizes)
             c.set_window_centre("intlen")
     autotuned = None
@@ -1149,7 +1147,7 @@ def main():
                                  % (1024 // tun["window_sub"], tun["zero_window"], " (autotuned)" if autotuned else ""),
                         "conv": ("k_conv_blk (extension: separable Gaussian convolution, LDS-staged %d-row x "
                                  "%d-column block tiles on %d waves, DPP lane shifts, store pace %s)"
-                                 % (ctx.tuning()["conv_rows"], 4 * (64 - 2 * ctx.tuning()["conv_halo"]),
+                                 % (ctx.tuning()["conv_rows"], 240,
                                     ctx.tuning().get("conv_waves") or 16,
                                     "off" if tun["conv_pace"] < 0 else "vmcnt(%d)" % tun["conv_pace"])
                                  if ctx.tuning()["conv_kernel"] == 2 and S <= 5 else
@@ -1173,7 +1171,7 @@ def main():
             else None), "rounds": 5}
     result["tuning"] = {k: tun[k] for k in ("variant", "tile_order", "zero_window", "store_pace", "inplace_sub",
                                             "window_sub", "inplace_pace", "conv_kernel", "conv_rows", "conv_order",
-                                            "conv_waves", "conv_halo", "conv_pace", "pyramid_chunk_kb") if k in tun}
+                                            "conv_waves", "conv_pace", "pyramid_chunk_kb") if k in tun}
     result["topology"] = topology
     if distribution is not None:
         result["distribution"] = distribution

@@ -345,12 +345,9 @@ enum {
     GDP_TUNE_INPLACE_PACE = 19, /* the same for the in-place re-entry (gdp_generate_dog, k_levels;
                                    default -1): its own field, so tuning the build's pacing never
                                    changes the in-place passes' speed */
-    GDP_TUNE_PYRAMID_CHUNK_KB = 20, /* read-only: how the context-owned pyramid is backed — KiB per
+    GDP_TUNE_PYRAMID_CHUNK_KB = 20 /* read-only: how the context-owned pyramid is backed — KiB per
                                       separately created physical piece (default 2 MiB, at most
                                       4096 pieces), -1 one piece per image, 0 one hipMalloc */
-    GDP_TUNE_CONV_HALO = 21     /* gdp_build_gaussian block tiles (16 waves): lanes at each end of a
-                                   wave that only stage halo columns — 2 (240-column tiles), 4 (224:
-                                   line-aligned stores), 8 (192: line-aligned loads and stores) */
 };
 int gdp_set_tuning(gdp_ctx* ctx, int key, int value);
 /* The build-kernel variant ids this library holds (GDP_TUNE_VARIANT values): writes up to

@@ -30,7 +30,6 @@ GDP_TUNE_STORE_PACE = 17
 GDP_TUNE_CONV_PACE = 18
 GDP_TUNE_INPLACE_PACE = 19
 GDP_TUNE_PYRAMID_CHUNK_KB = 20
-GDP_TUNE_CONV_HALO = 21
 
 
 class GdpError(RuntimeError):

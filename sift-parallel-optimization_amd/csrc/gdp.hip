@@ -438,7 +438,7 @@ static void conv_sweep_geom(gdp_ctx* c) {
         const long long rows_per_blk = (long long)kSwWaves * conv_sweep_rows(c);
         g.sw_blk[o + 1] = g.sw_blk[o] + (sweep ? (unsigned)((og.rows + rows_per_blk - 1) / rows_per_blk * g.sw_strips_c[o]) : 0u);
         const long long bk_rows = c->conv_rows;
-        const int bk_cols = 4 * (64 - 2 * g.bk_halo_lanes);  // block-tile output columns (240 / 224 / 192)
+        const int bk_cols = 4 * (64 - 2 * kBkHaloLanes);  // block-tile output columns (240)
         g.bk_strips_c[o] = (og.cols + bk_cols - 1) / bk_cols;
         g.bk_blk[o + 1] = g.bk_blk[o] + (sweep ? (unsigned)((og.rows + bk_rows - 1) / bk_rows * g.bk_strips_c[o]) : 0u);
         g.cvx_blk[o + 1] = g.cvx_blk[o] + (sweep ? 0u : g.cv_blk[o + 1] - g.cv_blk[o]);
@@ -511,9 +511,9 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int L, int T, int W, int HL = 2>
+template <int L, int T, int W>
 hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
-    auto k = k_conv_blk<L, T, W, HL>;
+    auto k = k_conv_blk<L, T, W, kBkHaloLanes>;
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
                        c->d_conv_perm);
@@ -527,7 +527,6 @@ template <int L>
 hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
     const int T = c->conv_rows, W = c->conv_waves;
     if (W == 8) {
-        if (c->geom.bk_halo_lanes != 2) return hipErrorInvalidConfiguration;  // 8 waves: 240-column tiles only
         switch (T) {
             case 8: return launch_conv_blk_t<L, 8, 8>(c, units, st);
             case 16: return launch_conv_blk_t<L, 16, 8>(c, units, st);
@@ -537,17 +536,10 @@ hipError_t launch_conv_blk(gdp_ctx* c, unsigned units, hipStream_t st) {
         }
     }
     if (W != 16) return hipErrorInvalidConfiguration;
-    // 16 waves: halo lanes 2 (240-column tiles), 4 (224) or 8 (192, line-aligned loads and stores)
-    switch (T * 16 + c->geom.bk_halo_lanes) {
-        case 16 * 16 + 2: return launch_conv_blk_t<L, 16, 16, 2>(c, units, st);
-        case 32 * 16 + 2: return launch_conv_blk_t<L, 32, 16, 2>(c, units, st);
-        case 48 * 16 + 2: return launch_conv_blk_t<L, 48, 16, 2>(c, units, st);
-        case 16 * 16 + 4: return launch_conv_blk_t<L, 16, 16, 4>(c, units, st);
-        case 32 * 16 + 4: return launch_conv_blk_t<L, 32, 16, 4>(c, units, st);
-        case 48 * 16 + 4: return launch_conv_blk_t<L, 48, 16, 4>(c, units, st);
-        case 16 * 16 + 8: return launch_conv_blk_t<L, 16, 16, 8>(c, units, st);
-        case 32 * 16 + 8: return launch_conv_blk_t<L, 32, 16, 8>(c, units, st);
-        case 48 * 16 + 8: return launch_conv_blk_t<L, 48, 16, 8>(c, units, st);
+    switch (T) {
+        case 16: return launch_conv_blk_t<L, 16, 16>(c, units, st);
+        case 32: return launch_conv_blk_t<L, 32, 16>(c, units, st);
+        case 48: return launch_conv_blk_t<L, 48, 16>(c, units, st);
         default: return hipErrorInvalidConfiguration;
     }
 }
@@ -881,7 +873,6 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // the convolution block tiles' five stores per output row go out back to back; vmcnt(2) after
     // each measured 0.5-1.3 % faster on 4096^2 / 64 x 4096^2 / 16384^2 (profiles/sp_conv_c*_r03ap.log)
     g.conv_pace = 2;
-    g.bk_halo_lanes = 2;
     c->in_pitch_own = g.in_pitch;
     c->in_img_stride_own = g.in_img_stride;
 
@@ -2061,7 +2052,6 @@ int gdp_get_tuning(const gdp_ctx* c, int key, int* value) try {
         case GDP_TUNE_STORE_PACE: *value = c->geom.store_pace; return GDP_OK;
         case GDP_TUNE_INPLACE_PACE: *value = c->geom.inplace_pace; return GDP_OK;
         case GDP_TUNE_CONV_PACE: *value = c->geom.conv_pace; return GDP_OK;
-        case GDP_TUNE_CONV_HALO: *value = c->geom.bk_halo_lanes; return GDP_OK;
         case GDP_TUNE_BUILD_LDS: *value = c->build_lds; return GDP_OK;
         case GDP_TUNE_STAGE_KB: *value = (int)(c->stage_half_floats / 256); return GDP_OK;
         case GDP_TUNE_STAGE_THREADS: *value = c->stage_threads; return GDP_OK;
@@ -2108,8 +2098,6 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
         }
         case GDP_TUNE_CONV_WAVES:
             if (value != 8 && value != 16) return c->status(GDP_ERR_ARG, "conv waves must be 8 or 16");
-            if (value == 8 && c->geom.bk_halo_lanes != 2)
-                return c->status(GDP_ERR_ARG, "8-wave block tiles take halo lanes 2 only (GDP_TUNE_CONV_HALO)");
             c->conv_waves = value;
             return conv_follow_rows(c);
         case GDP_TUNE_STORE_PACE:
@@ -2140,21 +2128,6 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
             if (value < 0 || value > 7) return c->status(GDP_ERR_ARG, "conv order must be 0..7");
             c->conv_order = value;
             return GDP_OK;
-        case GDP_TUNE_CONV_HALO: {
-            if (value != 2 && value != 4 && value != 8)
-                return c->status(GDP_ERR_ARG, "conv halo lanes must be 2 (240-column block tiles), 4 (224) or 8 (192)");
-            if (value != 2 && c->conv_waves != 16)
-                return c->status(GDP_ERR_ARG, "conv halo lanes 4 / 8 need 16-wave block tiles");
-            const int old = c->geom.bk_halo_lanes;
-            c->geom.bk_halo_lanes = value;
-            conv_sweep_geom(c);
-            const int rc = upload_geom(c);
-            if (rc != GDP_OK) {
-                c->geom.bk_halo_lanes = old;
-                conv_sweep_geom(c);
-            }
-            return rc;
-        }
         case GDP_TUNE_BUILD_LDS:
             if (value < 0 || value > 160 * 1024) return c->status(GDP_ERR_ARG, "build LDS bytes must be in [0, 163840]");
             c->build_lds = value;

@@ -262,7 +262,7 @@ class PyramidContext:
 
     _TUNING = ("nontemporal", "blocks_per_cu", "grid", "variant", "tile_order", "inplace_sub", "window_sub",
                "conv_kernel", "conv_rows", "conv_order", "build_lds", "stage_kb", "stage_threads", "conv_waves", "zero_window",
-               "store_pace", "conv_pace", "inplace_pace", "conv_halo", "pyramid_chunk_kb")  # the last one read-only
+               "store_pace", "conv_pace", "inplace_pace", "pyramid_chunk_kb")  # the last one read-only
 
     @staticmethod
     def _tuning_key(name):
@@ -273,7 +273,7 @@ class PyramidContext:
     def set_tuning(self, nontemporal=None, blocks_per_cu=None, grid=None, variant=None, tile_order=None,
                    inplace_sub=None, window_sub=None, conv_kernel=None, conv_rows=None, conv_order=None,
                    build_lds=None, stage_kb=None, stage_threads=None, conv_waves=None, zero_window=None,
-                   store_pace=None, conv_pace=None, inplace_pace=None, conv_halo=None):
+                   store_pace=None, conv_pace=None, inplace_pace=None):
         """Performance knobs of the kernels (outputs are bit-identical for every setting; the
         conv_* knobs select the convolution extension's kernel: 0 register sweep, 1 LDS tiles,
         2 block tiles, and the sweep's rows per wave strip (16 / 32) or the block tiles' rows per
@@ -282,13 +282,12 @@ class PyramidContext:
         size the double-buffered pinned staging of the row-pointer downloads; zero_window = 1 lets the
         build store the input-independent levels of pixels outside every window's support without
         waiting for their input; store_pace / conv_pace / inplace_pace pace the stores of the
-        builds / the convolution block tiles / the in-place re-entry, each its own field; conv_halo
-        = 2 / 4 / 8 halo lanes per 16-wave block-tile wave: 240- / 224- / 192-column tiles)."""
+        builds / the convolution block tiles / the in-place re-entry, each its own field)."""
         vals = dict(nontemporal=nontemporal, blocks_per_cu=blocks_per_cu, grid=grid, variant=variant,
                     tile_order=tile_order, inplace_sub=inplace_sub, window_sub=window_sub, conv_kernel=conv_kernel,
                     conv_rows=conv_rows, conv_order=conv_order, build_lds=build_lds, stage_kb=stage_kb,
                     stage_threads=stage_threads, conv_waves=conv_waves, zero_window=zero_window,
-                    store_pace=store_pace, conv_pace=conv_pace, inplace_pace=inplace_pace, conv_halo=conv_halo)
+                    store_pace=store_pace, conv_pace=conv_pace, inplace_pace=inplace_pace)
         for name, val in vals.items():
             if val is not None:
                 check(lib().gdp_set_tuning(self._ctx, self._tuning_key(name), int(val)), self._ctx)
