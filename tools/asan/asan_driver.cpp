@@ -105,6 +105,31 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
         EXPECT(gdp_upload_level(c, 0, go, 0, raw.data()) == GDP_ERR_ARG);
         OK(gdp_gauss_scales(c, 1, 2, 0, go, nullptr));
         EXPECT(gdp_gauss_scales(c, 2, 2, 0, go, nullptr) == GDP_ERR_ARG);
+        // round 5: the pipelined mirrored GenerateDoG (pageable and pinned host buffers) == the
+        // serial upload + in-place pass + download
+        OK(gdp_download_image_raw(c, 0, raw.data()));
+        std::vector<float> piped(raw);
+        OK(gdp_generate_dog_mirrored(c, 0, piped.data()));
+        OK(gdp_upload_image_raw(c, 0, raw.data()));
+        OK(gdp_generate_dog(c, nullptr));
+        std::vector<float> serial(raw.size());
+        OK(gdp_download_image_raw(c, 0, serial.data()));
+        for (int o = 0; o < go; ++o)
+            for (int s = 0; s < gs + 3; ++s) {
+                int lr, lc, first;
+                OK(gdp_level_dims(c, o, &lr, &lc, &first));
+                const size_t off = gdp_level_offset(c, 0, o, s);
+                EXPECT(std::memcmp(piped.data() + off, serial.data() + off, (size_t)lr * lc * 4) == 0);
+            }
+        void* pinned = nullptr;
+        OK(gdp_host_alloc(raw.size() * 4, &pinned));
+        std::memcpy(pinned, raw.data(), raw.size() * 4);
+        OK(gdp_generate_dog_mirrored(c, 0, static_cast<float*>(pinned)));
+        gdp_host_free(pinned);
+        EXPECT(gdp_generate_dog_mirrored(c, 1 << 20, raw.data()) == GDP_ERR_ARG);
+        EXPECT(gdp_generate_dog_mirrored(c, 0, nullptr) == GDP_ERR_ARG);
+        int ids[64];
+        EXPECT(gdp_build_variants(ids, 64) == gdp_build_variants(nullptr, 0));
     }
     OK(gdp_gauss_range(c, 0, go, nullptr));
     // tuning: every key, valid and invalid values

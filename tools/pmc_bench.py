@@ -44,10 +44,16 @@ def main():
     ap.add_argument("--round", required=True)
     ap.add_argument("--tag", required=True)
     args = ap.parse_args()
-    fs = per_dispatch(args.fetch, "FETCH_SIZE", args.kernel)
-    ws = per_dispatch(args.write, "WRITE_SIZE", args.kernel)
+    kernel = args.kernel
+    if kernel == "from-bench":  # exactly the instance the bench line timed (the autotune ran others)
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from timed_dispatches import instance_name
+
+        kernel = instance_name(json.loads([x for x in open(args.bench_log) if x.startswith("{")][-1])["roofline"]["kernel"])
+    fs = per_dispatch(args.fetch, "FETCH_SIZE", kernel)
+    ws = per_dispatch(args.write, "WRITE_SIZE", kernel)
     if not fs or not ws:
-        sys.exit(f"no {args.kernel} dispatches in the PMC output")
+        sys.exit(f"no {kernel} dispatches in the PMC output")
     line = [x for x in open(args.bench_log) if x.startswith("{")][-1]
     bench = json.loads(line)
     roof = bench["roofline"]

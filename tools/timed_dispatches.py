@@ -26,6 +26,16 @@ VARIANTS = {0: (1024, 256, 0, 16), 8: (512, 256, 0, 8), 11: (768, 384, 0, 8), 15
             23: (768, 768, 4, 0), 27: (512, 512, 5, 0)}
 
 
+def instance_name(kernel_string):
+    """The kernel-trace name fragment of the instance a bench line's roofline.kernel names."""
+    m = re.search(r"variant (\d+)", kernel_string)
+    if kernel_string.startswith("k_build") and m:
+        blk, tc, path, tr = VARIANTS[int(m.group(1))]
+        sub = "true" if "SUB" in kernel_string.split(" ")[0] else "false"
+        return f"k_build<5, true, {blk}, {tc}, {path}, {tr}, {sub}>"
+    return kernel_string.split(" ")[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", required=True, help="rocprofv3 -d directory of the --kernel-trace run")
@@ -33,15 +43,8 @@ def main():
     ap.add_argument("--tag", required=True)
     args = ap.parse_args()
     line = json.loads([x for x in open(args.bench_log) if x.startswith("{")][-1])
-    kern = line["roofline"]["kernel"]
     steps = line["steps"]
-    m = re.search(r"variant (\d+)", kern)
-    if kern.startswith("k_build") and m:
-        blk, tc, path, tr = VARIANTS[int(m.group(1))]
-        sub = "true" if "SUB" in kern.split(" ")[0] else "false"
-        want = f"k_build<5, true, {blk}, {tc}, {path}, {tr}, {sub}>"
-    else:
-        want = kern.split(" ")[0]
+    want = instance_name(line["roofline"]["kernel"])
     rows = []
     for p in glob.glob(os.path.join(args.trace, "**", "*kernel_trace.csv"), recursive=True):
         with open(p) as f:
