@@ -140,7 +140,12 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
     EXPECT(gdp_set_tuning(c, GDP_TUNE_VARIANT, 99) != GDP_OK);
     EXPECT(gdp_set_tuning(c, GDP_TUNE_CONV_ROWS, 7) != GDP_OK);
     EXPECT(gdp_set_tuning(c, 12345, 0) != GDP_OK);
-    for (int v = 0; v < 9; ++v) OK(gdp_set_tuning(c, GDP_TUNE_VARIANT, v));
+    {  // every variant the library holds, and a removed id refused
+        int ids[64];
+        const int nv = gdp_build_variants(ids, 64);
+        for (int i = 0; i < nv && i < 64; ++i) OK(gdp_set_tuning(c, GDP_TUNE_VARIANT, ids[i]));
+        EXPECT(gdp_set_tuning(c, GDP_TUNE_VARIANT, 1) == GDP_ERR_ARG);
+    }
     int bv = -1, bo = -1;
     float bms = 0;
     OK(gdp_autotune(c, 1, nullptr, &bv, &bo, &bms));
