@@ -1,0 +1,56 @@
+"""The evidence trail resolves: every profiles/ file DESIGN.md, README.md and
+INTEGRATION.md cite — by path or as a backticked file name, brace sets and globs expanded — is a
+tracked file under profiles/, and the directory stays small."""
+import fnmatch
+import os
+import re
+import subprocess
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _expand(ref):
+    b = re.search(r"\{([^}]*)\}", ref)
+    if not b:
+        return [ref]
+    out = []
+    for x in b.group(1).split(","):
+        out += _expand(ref[:b.start()] + x + ref[b.end():])
+    return out
+
+
+def _cited(text):
+    refs = set()
+    for m in re.finditer(r"profiles/([A-Za-z0-9_.{},*\-]+)", text):
+        refs.add(m.group(1).rstrip(".,)"))
+    for m in re.finditer(r"`([A-Za-z0-9_{},*\-]+(?:\.[a-z0-9]+)*\.(?:log|json|csv))`", text):
+        refs.add(m.group(1))
+    return refs
+
+
+def test_every_cited_profile_exists():
+    tracked = subprocess.run(["git", "ls-files", "profiles"], cwd=REPO, capture_output=True, text=True,
+                             check=True).stdout.split()
+    names = {os.path.relpath(p, "profiles") for p in tracked} | set(os.listdir(os.path.join(REPO, "profiles")))
+    import json  # PMC records gathered into profiles/pmc_records.json keep their file names
+
+    with open(os.path.join(REPO, "profiles", "pmc_records.json")) as f:
+        names |= {r["file"] for r in json.load(f)}
+    missing = []
+    for doc in ("DESIGN.md", "README.md", "INTEGRATION.md"):
+        text = open(os.path.join(REPO, doc)).read()
+        for ref in _cited(text):
+            if ref.startswith(("pmc_records.json#", "archive_")) or "/" in ref.rstrip("/"):
+                continue
+            if ref.endswith(".json") and not ref.startswith(("pmc_", "sq_", "calib_")):
+                continue  # repo-level JSON (BENCH_r04.json, meta.json, ...) is not a profile
+            for alt in _expand(ref):
+                if not any(fnmatch.fnmatch(n, alt) for n in names):
+                    missing.append((doc, alt))
+    assert not missing, missing
+
+
+def test_profiles_directory_stays_small():
+    tracked = subprocess.run(["git", "ls-files", "profiles"], cwd=REPO, capture_output=True, text=True,
+                             check=True).stdout.split()
+    assert len(tracked) < 400, len(tracked)
