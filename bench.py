@@ -819,8 +819,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="override images per GPU")
-    ap.add_argument("--image-stride-mb", type=int, default=None,
-                    help="spread layout: images this many MiB apart (GDP_IMAGE_STRIDE_MB; DESIGN.md §5.1)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=None,
@@ -868,9 +866,6 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the N ranks here, before torch is imported or a GPU is touched
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    if args.image_stride_mb:
-        os.environ["GDP_IMAGE_STRIDE_MB"] = str(args.image_stride_mb)  # read when each context is created
-
     import torch
 
     import __graft_entry__ as entry

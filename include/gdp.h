@@ -86,14 +86,14 @@ void gdp_destroy(gdp_ctx* ctx);
 int gdp_get_geometry(const gdp_ctx* ctx, int* height, int* width, int* S, int* octaves, int* batch);
 int gdp_level_dims(const gdp_ctx* ctx, int octave, int* rows, int* cols, int* first_row);
 size_t gdp_pyramid_bytes(const gdp_ctx* ctx); /* device bytes of all pyramids of the batch */
-/* Layout knobs read from the environment when a context is created (experiments; every setting
- * gives identical bits): GDP_LEVEL_PAD (floats between levels), GDP_ROWTAP_LAYOUT (non-square row
- * windows [row][scale] = 1 / [scale][row] = 0), GDP_IMAGE_STRIDE_MB (images at least this many MiB
- * apart: the "spread" layout of DESIGN.md §5.1, which lets tile order 1's eight XCD ranges of a
- * batch lie gigabytes apart), GDP_SPREAD_VMM = 1 (the pyramid as a reserved address range with one
- * physical chunk mapped per image; the gaps stay unmapped) with GDP_SPREAD_PHYS_MB (physical
- * spacer created after each chunk and released once all are mapped).  gdp_pyramid_bytes and
- * gdp_level_offset follow the spread stride; gdp_image_floats stays one image's dense extent. */
+/* The pyramid's backing: by default one reserved address range backed by separately
+ * created 2 MiB physical pieces (GDP_TUNE_PYRAMID_CHUNK_KB reports it); GDP_SPREAD_VMM=0 in the
+ * environment when the context is created gives one hipMalloc instead (e.g. to share the pyramid
+ * with another process through IPC).  Identical bits and offsets either way.  Each image starts
+ * on an allocation granule only where that wastes at most 1/16 of an image: gdp_pyramid_bytes and
+ * gdp_level_offset follow that stride, gdp_image_floats stays one image's dense extent.  (The
+ * layout experiments of DESIGN.md §4 read further variables only in the research build,
+ * `make -C sift-parallel-optimization_amd/csrc exp`.) */
 
 /* ---- input ---------------------------------------------------------------------------------
  * The reference deep-copies `int** img` in its constructor (GuassDePyramid.h:38-46).  These
