@@ -1,0 +1,7 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gputest_r05h.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as e; e.smoke(); print('smoke ok')" > gpurun_out/smoke_r05h.log 2>&1
+timeout -k 10 400 python bench.py > gpurun_out/bench_default_r05h.log 2>&1
+timeout -k 10 600 make -C tools/asan run > gpurun_out/asan_r05h.log 2>&1
+echo done

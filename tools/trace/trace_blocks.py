@@ -2,6 +2,7 @@
 """Ramp and tail of one cold k_build launch, from per-block timestamps (diagnostic build).
 
     make -C tools/trace && python tools/trace/trace_blocks.py [--shape 4096x4096x1] [--variant 0]
+    python tools/trace/trace_blocks.py --op conv [--conv-rows 48 --conv-waves 16]   (k_conv_blk)
 
 Builds tools/trace/libgdp_trace.so's k_build over `--rotate` buffer sets (so the traced launch is
 cold, as in bench.py), then traces one launch: per WAVE the 100 MHz real-time clock at entry and
@@ -29,6 +30,10 @@ def main():
     ap.add_argument("--store-pace", type=int, default=-1)
     ap.add_argument("--order", type=int, default=0)
     ap.add_argument("--rotate", type=int, default=5)
+    ap.add_argument("--op", choices=("build", "conv"), default="build")
+    ap.add_argument("--conv-rows", type=int, default=None)
+    ap.add_argument("--conv-waves", type=int, default=None)
+    ap.add_argument("--conv-order", type=int, default=None)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -44,11 +49,16 @@ def main():
     ctxs = [pkg.PyramidContext(H, W, S=2, octaves=5, batch=B) for _ in range(args.rotate)]
     for c in ctxs:
         c.fill_synthetic(0x5EED, 0)
-        c.set_tuning(variant=args.variant, tile_order=args.order, zero_window=args.zero_window,
-                     store_pace=args.store_pace)
+        if args.op == "conv":
+            c.set_tuning(conv_kernel=2, conv_rows=args.conv_rows, conv_waves=args.conv_waves,
+                         conv_order=args.conv_order)
+        else:
+            c.set_tuning(variant=args.variant, tile_order=args.order, zero_window=args.zero_window,
+                         store_pace=args.store_pace)
+    run = (lambda c, st=None: c.build_gaussian(st)) if args.op == "conv" else (lambda c, st=None: c.build(st))
     for _ in range(3):
         for c in ctxs:
-            c.build()
+            run(c)
     for c in ctxs:
         c.sync()
     blocks = 1 << 24  # wave records
@@ -56,15 +66,23 @@ def main():
     out = []
     for rep in range(3):
         for c in ctxs[1:]:
-            c.build()
+            run(c)
         for c in ctxs:
             c.sync()
         buf.zero_()
         torch.cuda.synchronize()
         assert lib.gdp_debug_set_block_trace(ctypes.c_void_p(buf.data_ptr())) == 0
         ev_ms = ctypes.c_float()
-        # one traced launch between HIP events on the context's stream (gdp_time_builds, iters 1)
-        assert lib.gdp_time_builds(ctxs[0]._ctx, 1, None, ctypes.byref(ev_ms)) == 0
+        if args.op == "conv":  # one traced launch between torch events on torch's current stream
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            run(ctxs[0], st)
+            e1.record(st)
+            e1.synchronize()
+            ev_ms.value = e0.elapsed_time(e1)
+        else:  # one traced launch between HIP events on the context's stream (gdp_time_builds, iters 1)
+            assert lib.gdp_time_builds(ctxs[0]._ctx, 1, None, ctypes.byref(ev_ms)) == 0
         ctxs[0].sync()
         assert lib.gdp_debug_set_block_trace(None) == 0
         t = buf.cpu().numpy().reshape(-1, 3)
