@@ -12,8 +12,11 @@
 // default, csrc/gdp.hip alloc_spread); "malloc" = one hipMalloc.  Launches rotate over 5 buffer
 // sets (2.57 GB, beyond the 256 MB Infinity Cache) as bench.py does; each launch is timed alone
 // with HIP events.  Cases: ideal build per image (config 2's launch), the same kernel over 16
-// images in one launch (a long launch, config 4's regime), and a write-only stream of the same
-// 514,064,384 B.  One JSON line per case.
+// images in one launch (a long launch, config 4's regime), a write-only stream of the same
+// 514,064,384 B, and — for the in-place re-entry pass `k_levels` (`--op regen`) — an in-place
+// read-modify-write of the 447 MB pyramid: one thread per 4-pixel group loading its five levels,
+// then storing five (k_levels' shape without the windows), in 256-thread blocks.  One JSON line
+// per case.
 //   make -C tools sol_c2 && tools/sol_c2 [launches]
 #include <hip/hip_runtime.h>
 
@@ -56,6 +59,18 @@ __global__ void __launch_bounds__(1024) k_ideal(const i4* __restrict__ in, f4* _
     for (int s = 0; s < 5; ++s) __builtin_nontemporal_store(v * (float)(s + 1), o + s * (kPix / 4) + t);
     f4* r = o + 5 * (kPix / 4) + (long)blockIdx.x * kRestPerBlock;
     for (int i = threadIdx.x; i < kRestPerBlock; i += 1024) __builtin_nontemporal_store(v, r + i);
+}
+
+// in-place five-level read-modify-write (k_levels' access shape): thread = one float4 of each level
+__global__ void __launch_bounds__(256) k_rmw5(f4* __restrict__ pyr, long lev_f4, long n) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    f4 v[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) v[s] = __builtin_nontemporal_load(pyr + s * lev_f4 + i);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) __builtin_nontemporal_store(v[s] - v[s + 1], pyr + s * lev_f4 + i);
+    __builtin_nontemporal_store(v[4], pyr + 4 * lev_f4 + i);
 }
 
 // write-only: one float4 per thread, 1024-thread blocks
@@ -165,6 +180,14 @@ int main(int argc, char** argv) {
                                reinterpret_cast<f4*>(out_base + slot * kOut), wn);
         };
         report("write_only_1img", bname, 1, (double)(kIn + kOut), time_launches(wonly, launches));
+        // the pyramid as five equal levels of kOut / 5 bytes, read and rewritten in place
+        const long lev = kOut / 5 / 16;
+        auto rmw = [&](int i) {
+            const long slot = (long)(i % sets) * 3;
+            hipLaunchKernelGGL(k_rmw5, dim3((unsigned)((lev + 255) / 256)), dim3(256), 0, 0,
+                               reinterpret_cast<f4*>(out_base + slot * kOut), lev, lev);
+        };
+        report("inplace_rmw5_1img", bname, 1, 2.0 * (double)kOut, time_launches(rmw, launches));
         CHECK(hipDeviceSynchronize());
         if (backing == 1) {
             CHECK(hipFree(in_base));
