@@ -1877,6 +1877,18 @@ int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
         c->ev_mirror.push_back(e);
     }
     hipEvent_t* ev = c->ev_mirror.data();
+    // an error after the first copy was queued returns only once every queued copy and pass has
+    // finished, so the caller never frees or reuses `host` under a DMA still in flight
+    struct DrainOnError {
+        gdp_ctx* c;
+        bool armed = true;
+        ~DrainOnError() {
+            if (!armed) return;
+            (void)hipStreamSynchronize(c->st_up);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->st_down);
+        }
+    } drain{c};
     // the uploads overwrite levels earlier work on the context's stream may still use
     GDP_HIP(c, hipEventRecord(ev[2 * chunks.size()], c->stream));
     GDP_HIP(c, hipStreamWaitEvent(c->st_up, ev[2 * chunks.size()], 0));
@@ -1904,6 +1916,7 @@ int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
     }
     GDP_HIP(c, hipStreamSynchronize(c->st_down));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
+    drain.armed = false;
     return GDP_OK;
 } GDP_ABI_CATCH(c)
 

@@ -300,6 +300,7 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
     if (gdp_get_geometry(band ? band : full, &H, &W, &S, &O, &B) != GDP_OK) {
         if (band || c->rank == root) return fail(c, GDP_ERR_ARG, "band geometry");
     }
+    if (band && (band_image < 0 || band_image >= B)) return fail(c, GDP_ERR_ARG, "gdp_comm_gather_bands: band_image out of range");
     if (c->rank == root) {
         int H2, W2, S2, O2, B2;
         gdp_get_geometry(full, &H2, &W2, &S2, &O2, &B2);
@@ -307,6 +308,7 @@ int gdp_comm_gather_bands(gdp_comm* c, gdp_ctx* band, int band_image, gdp_ctx* f
         gdp_level_dims(full, 0, &rows0, &cols0, &first0);
         if (H2 != H || W2 != W || S2 != S || O2 != O || first0 != 0 || rows0 != H)
             return fail(c, GDP_ERR_ARG, "collector context must be the whole image of the same geometry");
+        if (full_image < 0 || full_image >= B2) return fail(c, GDP_ERR_ARG, "gdp_comm_gather_bands: full_image out of range");
     }
     GDP_HIPC(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)gdp_stream(band ? band : full);

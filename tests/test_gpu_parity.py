@@ -1302,6 +1302,11 @@ def test_comm_failure_closes_the_group_and_fails_fast(pkg):
                 L.gdp_comm_destroy(bad)  # aborts the failed communicator
                 comm = new_comm()
                 assert L.gdp_comm_check(comm, None) == 0, L.gdp_comm_last_error(comm)  # RCCL still runs here
+            # image indices outside either context are refused before any transfer (GDP_ERR_ARG);
+            # the communicator stays usable
+            assert L.gdp_comm_gather_bands(comm, ctx._ctx, 1, full._ctx, 0, 0, None) == 1
+            assert L.gdp_comm_gather_bands(comm, ctx._ctx, 0, full._ctx, -1, 0, None) == 1
+            assert L.gdp_comm_failed(comm) == 0
             # the same collective on the fresh communicator succeeds and leaves the build intact
             assert L.gdp_comm_gather_bands(comm, ctx._ctx, 0, full._ctx, 0, 0, None) == 0, L.gdp_comm_last_error(comm)
             assert full.checksum(0) == want
