@@ -15,8 +15,9 @@
 // images in one launch (a long launch, config 4's regime), a write-only stream of the same
 // 514,064,384 B, and — for the in-place re-entry pass `k_levels` (`--op regen`) — an in-place
 // read-modify-write of the 447 MB pyramid: one thread per 4-pixel group loading its five levels,
-// then storing five (k_levels' shape without the windows), in 256-thread blocks.  One JSON line
-// per case.
+// then storing five (k_levels' shape without the windows), in 256-thread blocks; and a read-reuse
+// probe (a 1 MiB / 64 MiB working set read 64 times per thread) that shows whether each backing
+// is cached in L2 at all.  One JSON line per case.
 //   make -C tools sol_c2 && tools/sol_c2 [launches]
 #include <hip/hip_runtime.h>
 
@@ -71,6 +72,19 @@ __global__ void __launch_bounds__(256) k_rmw5(f4* __restrict__ pyr, long lev_f4,
 #pragma unroll
     for (int s = 0; s < 4; ++s) __builtin_nontemporal_store(v[s] - v[s + 1], pyr + s * lev_f4 + i);
     __builtin_nontemporal_store(v[4], pyr + 4 * lev_f4 + i);
+}
+
+// cache probe: every thread reads `reps` float4s from a small working set (`ws` float4s, e.g. 1 MiB):
+// served from L2 when the backing is cached there, from memory when it is not
+__global__ void __launch_bounds__(256) k_reuse(const f4* __restrict__ p, long ws, int reps, float* sink) {
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    long i = ((long)blockIdx.x * 256 + threadIdx.x) % ws;
+    for (int r = 0; r < reps; ++r) {
+        acc += p[i];
+        i += 4099 * 64;  // next line of another wave's block, wrapping in the working set
+        if (i >= ws) i -= ws;
+    }
+    if (acc.x + acc.y + acc.z + acc.w == 1234.5f) sink[0] = 1.f;
 }
 
 // write-only: one float4 per thread, 1024-thread blocks
@@ -188,6 +202,18 @@ int main(int argc, char** argv) {
                                reinterpret_cast<f4*>(out_base + slot * kOut), lev, lev);
         };
         report("inplace_rmw5_1img", bname, 1, 2.0 * (double)kOut, time_launches(rmw, launches));
+        // L2 residency of the backing: 1 MiB and 64 MiB working sets read 64 times per thread
+        for (long ws_mib : {1L, 64L}) {
+            const long ws = (ws_mib << 20) / 16;
+            const unsigned grid = 8192;
+            const int reps = 64;
+            auto reuse = [&](int) {
+                hipLaunchKernelGGL(k_reuse, dim3(grid), dim3(256), 0, 0, reinterpret_cast<const f4*>(out_base), ws, reps,
+                                   reinterpret_cast<float*>(in_base));
+            };
+            report(ws_mib == 1 ? "reuse_read_1MiB_ws" : "reuse_read_64MiB_ws", bname, 0, 16.0 * grid * 256 * reps,
+                   time_launches(reuse, 50));
+        }
         CHECK(hipDeviceSynchronize());
         if (backing == 1) {
             CHECK(hipFree(in_base));
