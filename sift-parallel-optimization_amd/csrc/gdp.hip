@@ -659,11 +659,12 @@ static void free_pyramid(gdp_ctx* c) {
     c->pyr_chunk_kb = 0;
 }
 
-// GDP_SPREAD_VMM (layout): reserve the pyramid's address range and back it with
-// separately created physical chunks — one per image (default), or GDP_SPREAD_CHUNK_MB-sized pieces
-// of a dense batch.  With GDP_IMAGE_STRIDE_MB the images sit that far apart and the gaps stay
-// unmapped; GDP_SPREAD_PHYS_MB creates that much physical spacer after each chunk and releases the
-// spacers once everything is mapped.  Nothing but placement changes: same offsets, same bits.
+// The pyramid's default backing (GDP_SPREAD_VMM=0 opts out): reserve its address range
+// and back it with separately created 2 MiB physical pieces (larger past 4,096 pieces), created in
+// a fixed pseudo-random order.  Research builds (GDP_EXPERIMENTS) also take GDP_SPREAD_CHUNK_MB/_KB
+// (piece size; 0 = one piece per image), GDP_IMAGE_STRIDE_MB (images that far apart, the gaps left
+// unmapped), GDP_SPREAD_PHYS_MB (a physical spacer after each piece, released once all are mapped)
+// and GDP_SPREAD_PERM (creation order).  Nothing but placement changes: same offsets, same bits.
 static hipError_t alloc_spread(gdp_ctx* c, std::string& where) {
     Geom& g = c->geom;
     hipMemAllocationProp prop = {};
