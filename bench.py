@@ -244,6 +244,33 @@ def pmc_records():
 _PMC_CACHE = {}
 
 
+def concurrent_streams(ctxs, bytes_launch, n_streams=4, launches=200):
+    """Informational, after the timed region (never `value`): the serving mode of INTEGRATION §5 —
+    independent single-image builds of the rotated contexts launched round-robin on `n_streams`
+    torch streams, so one launch's drain overlaps the next one's ramp.  Ms per image over
+    `launches` builds (host clock around synchronizes), its fraction of 8 TB/s for the same
+    algorithmic bytes, and whether every context's checksum is unchanged."""
+    import torch
+
+    n_streams = max(1, min(n_streams, len(ctxs)))
+    sums = [c.checksum(0) for c in ctxs]
+    streams = [torch.cuda.Stream() for _ in range(n_streams)]
+    for it in range(2):  # a warm pass over every context, then the timed pass
+        k_max = len(ctxs) * 2 if it == 0 else launches
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(k_max):
+            ctxs[k % len(ctxs)].build(streams[k % n_streams])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    ms = dt * 1e3 / launches
+    return {"streams": n_streams, "contexts": len(ctxs), "launches": launches, "ms_per_image": round(ms, 6),
+            "frac_of_8TBps": round(bytes_launch / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 4),
+            "checksums_unchanged": all(c.checksum(0) == v for c, v in zip(ctxs, sums)),
+            "note": "informational: one image per launch, launches of different contexts overlapping on "
+                    "several streams (INTEGRATION §5); `value` and `roofline` time one launch at a time"}
+
+
 def dropin_call_cost(n=4096, calls=5):
     """Per-call cost of the C++ drop-in class (include/GaussDePyramid-HIP.h, main.cpp's timing loop:
     GenerateDoG() on the same object) through examples/state_hip, outside the timed region: with
@@ -1179,6 +1206,8 @@ def main():
                                      " [op=subset: GaussPyramid_a512omp::GenerateDoG_nomp_dynamic's output, the "
                                      "CPU baseline's own semantics]" if args.op == "subset" else
                                      f" [op={args.op}: in-place pass]")
+    if args.op == "build" and world == 1 and not cfg["band"] and B == 1 and rotate > 1:
+        result["concurrent_streams"] = concurrent_streams(ctxs, bytes_launch)
     complete_line(result, args, rank, world, dist, mg, red_dev, bytes_launch, wall)
     for c in ctxs:
         c.close()
