@@ -874,6 +874,9 @@ def main():
                     help="--op conv: 0 register sweep, 1 LDS tiles, 2 block tiles (default)")
     ap.add_argument("--conv-rows", type=int, default=None,
                     help="--op conv: block tiles' rows per block (48 default) / the sweep's rows per strip (16/32)")
+    ap.add_argument("--conv-waves", type=int, default=None, choices=[8, 16],
+                    help="--op conv: waves per block tile (GDP_TUNE_CONV_WAVES; 16 waves: 16 / 32 / 48 rows, "
+                         "8 waves: 8 / 16 / 24 / 32 rows)")
     ap.add_argument("--conv-order", type=int, default=None,
                     help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
                          "after their input rows; default 4)")
@@ -990,7 +993,7 @@ def main():
         distribution = scatter_split(ctx, cfg, world, rank, dist, mg, backend, args.input)
     for c in ctxs:
         c.set_tuning(conv_kernel=args.conv_kernel, conv_rows=args.conv_rows, conv_order=args.conv_order,
-)
+                     conv_waves=args.conv_waves)
         if args.op == "subset":  # that header's integer-length window centre (the same taps at these sizes)
             c.set_window_centre("intlen")
     autotuned = None

@@ -514,6 +514,27 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
 template <int L, int T, int W>
 hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     auto k = k_conv_blk<L, T, W, kBkHaloLanes>;
+#ifdef GDP_EXPERIMENTS
+    // research A/B (S = 2 only): rows unrolled together x exact waves per SIMD (k_conv_blk_x)
+    if constexpr (L == 5 && T / W >= 2) {
+        static const int ur = [] { const char* e = std::getenv("GDP_CONV_UNROLL"); return e ? std::atoi(e) : 0; }();
+        static const int wv = [] { const char* e = std::getenv("GDP_CONV_WAVES_PER_SIMD"); return e ? std::atoi(e) : 8; }();
+        if (ur > 0) {
+            const int key = ur * 10 + wv;
+            switch (key) {
+                case 18: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 1, 8>; break;
+                case 16: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 1, 6>; break;
+                case 28: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 2, 8>; break;
+                case 26: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 2, 6>; break;
+                case 24: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 2, 4>; break;
+                case 38: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 3, 8>; break;
+                case 36: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 3, 6>; break;
+                case 34: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 3, 4>; break;
+                default: return hipErrorInvalidConfiguration;
+            }
+        }
+    }
+#endif
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
                        c->d_conv_perm);
