@@ -1314,6 +1314,24 @@ def test_comm_failure_closes_the_group_and_fails_fast(pkg):
         L.gdp_comm_destroy(comm)
 
 
+def test_cpp_serve_threads_contexts_are_independent(golden):
+    """examples/serve_threads: four host threads, one context (and stream) each, build their own
+    4096^2 synthetic images concurrently through the C ABI; every checksum equals a single
+    context's rebuild of that image AND the reference's own output for it
+    (tests/golden/checksums.json, synthetic images 0-3)."""
+    import json
+
+    exe = os.path.join(REPO, "examples", "serve_threads")
+    r = subprocess.run([exe, "4096", "4", "8"], timeout=120, capture_output=True, text=True)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["bit_identical_to_one_context"] is True
+    want = {int(c["input"].split(":")[2]): c["octaves_5"] for c in golden["checksums"]
+            if c["n"] == 4096 and c["S"] == 2 and c["input"].lower().startswith("synth:0x5eed:") and "octaves_5" in c}
+    for t, got in enumerate(line["checksums"]):
+        assert int(got, 16) == int(want[t], 16), (t, got, want[t])
+
+
 def test_cpp_conv_bands_mpi_example():
     """examples/conv_bands_mpi (MPI launcher + RCCL halo exchange + banded gdp_build_gaussian) as
     an MPI singleton and under mpiexec -n 1: the band checksums equal the whole image's."""
