@@ -321,9 +321,9 @@ enum {
                                    16 / 32 with 16 waves, 8 / 16 / 24 / 32 with 8); the sweep's
                                    rows per wave strip (16 / 32) */
     GDP_TUNE_CONV_ORDER = 11,   /* gdp_build_gaussian block order: bit 0 XCD-chunked, bit 1 odd
-                                   sweep waves go bottom-up (sweep only), bit 2 (default 4) octave
-                                   o's block rows issued right after the octave-0 rows covering
-                                   their input rows */
+                                   sweep waves go bottom-up (sweep only), bit 2 octave o's block
+                                   rows issued right after the octave-0 rows covering their input
+                                   rows.  Default 5 (4 for one image of >= 2^27 pixels) */
     GDP_TUNE_BUILD_LDS = 12,    /* gdp_build: dynamic LDS bytes requested per block (0 default);
                                    used only to cap resident blocks per CU (occupancy) */
     GDP_TUNE_STAGE_KB = 13,     /* row-pointer downloads: KiB per half of the double-buffered

@@ -863,8 +863,8 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // single images (4096^2 0.148 vs 0.152 ms for 256 threads, 16384^2 2.37 vs 2.49;
     // profiles/ab_sub_c*_r03m.log), 256-thread blocks on small batches, 1024-thread above
     c->inplace_sub = batch == 1 ? 16 : (long long)(row_end - row_begin) * W * batch <= (32ll << 20) ? 4 : 1;
-    // Convolution extension default: block tiles (16 waves) in block order 4 (octave-o block rows
-    // right after the octave-0 rows that hold their input rows, no XCD chunking) — the fastest form
+    // Convolution extension default: block tiles (16 waves) in block order 5 (below; octave-o block
+    // rows right after the octave-0 rows that hold their input rows, XCD-chunked) — the fastest form
     // on every config (tools/conv_ab.sh, cold buffers: 4096^2 0.111 ms vs 0.119 for the sweep,
     // 64 x 1080x1920 0.795 vs 0.809, 64 x 4096^2 6.34 vs 6.79, 16384^2 1.62 vs 1.72).  48 rows per
     // block since round 3: unpaced, 48 and 32 rows ran equal; with the stores paced at vmcnt(2)
@@ -872,7 +872,13 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
     // 64 x 4096^2 5.72 vs 5.92, 16384^2 1.461 vs 1.509; profiles/cpw_conv_c*_r03aw.log).
     c->conv_kernel = 2;
     c->conv_rows = 48;
-    c->conv_order = 4;
+    // Block order 5 (round 5): order 4's sequence XCD-chunked, so an octave-o block row runs on
+    // the XCD whose L2 has just staged its input rows — DRAM-bound reads halve (4096^2 162.4 ->
+    // 81.4 MB per launch, traffic 1.186 -> 1.036 x; 64 x 4096^2 1.185 -> 1.022 x) at the same
+    // speed (4096^2 0.1055-0.1060 vs 0.1058 ms, 64 x 4096^2 5.656-5.663 vs 5.631-5.674, 64 x
+    // 1080x1920 0.814-0.822 vs 0.808-0.811; profiles/conv_o{4,5}_c*_r05{v,w}.log).  A single image
+    // of >= 2^27 pixels keeps order 4: 16384^2 1.594-1.607 vs 1.623-1.633 ms in order 5.
+    c->conv_order = (batch == 1 && (long long)(row_end - row_begin) * W >= (1ll << 27)) ? 4 : 5;
     {
         const unsigned hw = std::thread::hardware_concurrency();
         if (hw > 0) c->stage_threads = std::max(1, std::min<int>(c->stage_threads, (int)hw));
