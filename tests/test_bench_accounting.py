@@ -234,6 +234,10 @@ def test_traffic_records_match_only_their_kernel_instance():
     for cfg in ("c2", "c4", "c5"):  # the round-3 default: 48-row block tiles
         rec = bench.latest_conv_pmc(cfg, {"conv_kernel": 2, "conv_rows": 48, "conv_order": 4})
         assert rec is not None and "k_conv_blk<5, 48, 16>" in rec["kernel"], cfg
+    for cfg in ("c2", "c3", "c4", "c5"):  # the round-5 default: block order 5 (order 4 kept for one huge image)
+        rec = bench.latest_conv_pmc(cfg, {"conv_kernel": 2, "conv_rows": 48, "conv_order": 5})
+        assert rec is not None and "k_conv_blk<5, 48, 16, 2>" in rec["kernel"], cfg
+        assert 0.99 < rec["traffic_over_algorithmic"] < (1.15 if cfg == "c5" else 1.05), (cfg, rec["traffic_over_algorithmic"])
     assert bench.latest_conv_pmc("c2", {"conv_kernel": 0, "conv_rows": 16, "conv_order": 0}) is None
 
 
