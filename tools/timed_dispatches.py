@@ -3,9 +3,11 @@
 
 bench.py's autotune and warm-up launch many kernel instances before the timed region, so the
 `--stats` average of an instance mixes them in.  The timed region is the LAST `steps` dispatches of
-the instance the bench line names (its kernel string: variant / tile order for k_build); this
-writes them as profiles/timed_dispatches_<tag>.csv (dispatch, start_ns, end_ns, duration_ns) and
-prints their mean next to the bench line's kernel_ms:
+the instance the bench line names (its kernel string: variant / tile order for k_build) on the
+bench's own stream — the stream that carries most of that instance's dispatches (the serving-mode
+`concurrent_streams` figure launches on four others); this writes them as
+profiles/timed_dispatches_<tag>.csv (dispatch, start_ns, end_ns, duration_ns) and prints their mean
+next to the bench line's kernel_ms:
 
     python3 tools/timed_dispatches.py --trace gpurun_out/prof_c2_trace --bench-log gpurun_out/prof_c2_trace.log \\
         --tag c2_r05e
@@ -50,15 +52,18 @@ def main():
         with open(p) as f:
             for r in csv.DictReader(f):
                 if want in r["Kernel_Name"]:
-                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                                 r.get("Stream_Id", "0")))
     rows.sort()
-    timed = rows[-steps:]
+    streams = [x[3] for x in rows]
+    main = max(set(streams), key=streams.count) if streams else None
+    timed = [x for x in rows if x[3] == main][-steps:]
     out = os.path.join(REPO, "profiles", f"timed_dispatches_{args.tag}.csv")
     with open(out, "w") as f:
         f.write("dispatch,start_ns,end_ns,duration_ns\n")
-        for i, (s, e, _) in enumerate(timed):
+        for i, (s, e, _, _) in enumerate(timed):
             f.write(f"{i},{s},{e},{e - s}\n")
-    d = [e - s for s, e, _ in timed]
+    d = [e - s for s, e, _, _ in timed]
     print(json.dumps({"file": os.path.relpath(out, REPO), "kernel": timed[0][2] if timed else want,
                       "dispatches": len(timed), "mean_us": round(statistics.mean(d) / 1e3, 3) if d else None,
                       "median_us": round(statistics.median(d) / 1e3, 3) if d else None,
