@@ -444,6 +444,32 @@ def launch_ranks(n, argv, script=None):
     return rc
 
 
+def gpu_state(pci):
+    """Clocks, power and temperatures of this rank's GPU right after its timed steps (`rocm-smi`,
+    informational: boxes of this part differ by up to +-3 % on the same command, and this is what
+    such a difference can be read against).  None when rocm-smi is missing or says nothing."""
+    import shutil
+    import subprocess
+
+    smi = shutil.which("rocm-smi") or ("/opt/rocm/bin/rocm-smi" if os.path.exists("/opt/rocm/bin/rocm-smi") else None)
+    if not smi:
+        return None
+    try:
+        r = subprocess.run([smi, "--showclocks", "--showpower", "--showtemp", "--showbus", "--json"],
+                           capture_output=True, text=True, timeout=20)
+        cards = json.loads(r.stdout[r.stdout.index("{"):])
+    except Exception:  # noqa: BLE001 - informational only
+        return None
+    card = next((v for v in cards.values() if isinstance(v, dict) and str(v.get("PCI Bus", "")).lower() == pci.lower()),
+                next(iter(cards.values())) if len(cards) == 1 else None)
+    if not isinstance(card, dict):
+        return None
+    keep = ("mclk clock speed:", "fclk clock speed:", "sclk clock speed:", "socclk clock speed:",
+            "Current Socket Graphics Package Power (W)", "Temperature (Sensor junction) (C)",
+            "Temperature (Sensor memory) (C)", "PCI Bus")
+    return {k.rstrip(":"): card[k] for k in keep if k in card} or None
+
+
 def rank_topology(world, rank, local, backend, dist, args):
     """Which device each rank drives, and how many ranks the collective backend sees — so an
     N-rank line proves "N ranks on N distinct GPUs" from its own record: every rank's device
@@ -1082,6 +1108,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # per-launch, HIP events on the launch stream
+    topology["gpu_state_after_timed_steps"] = gpu_state(topology["devices"][0]["pci"]) if rank == 0 else None
     if dist:  # every rank's own timing, recorded beside the max that the line reports
         per_rank = [None] * world
         dist.all_gather_object(per_rank, {"rank": rank, "ms_per_step": round(wall * 1e3 / args.steps, 6),
