@@ -274,25 +274,29 @@ def concurrent_streams(ctxs, bytes_launch, n_streams=4, launches=200):
 def dropin_call_cost(n=4096, calls=5):
     """Per-call cost of the C++ drop-in class (include/GaussDePyramid-HIP.h, main.cpp's timing loop:
     GenerateDoG() on the same object) through examples/state_hip, outside the timed region: with
-    the default two-way GaussPy (mirror_host: upload + in-place pass + download of the whole
-    pyramid over PCIe every call, pipelined over row chunks) and with mirror_host = false (the
-    device pyramid is the state; no PCIe).  ADVICE r4: the mirror's cost, measured."""
+    the default two-way GaussPy (mirror_host, write-tracked: the caller writes nothing, so only the
+    in-place pass and the pyramid's download over PCIe, pipelined over row chunks), with the write
+    tracking off (TrackWrites(false): the whole pyramid uploaded too, round 5's default) and with
+    mirror_host = false (the device pyramid is the state; no PCIe).  ADVICE r4 / VERDICT r5 item 2."""
     import re
     import subprocess
 
     exe = os.path.join(REPO, "examples", "state_hip")
     if not os.path.exists(exe):
         return None
-    out = {"n": n, "S": 2, "calls": calls, "source": "examples/state_hip hip <n> 2 ones - [mirror:0] dog time:<calls>"}
-    for key, ops in (("mirror_host_ms", []), ("device_state_ms", ["mirror:0"])):
+    out = {"n": n, "S": 2, "calls": calls,
+           "source": "examples/state_hip hip <n> 2 ones - [track:0 | mirror:0] dog time:<calls>"}
+    for key, ops in (("mirror_host_ms", []), ("mirror_untracked_ms", ["track:0"]), ("device_state_ms", ["mirror:0"])):
         # one untimed call first (the mirror's copy streams and events are created on first use)
         r = subprocess.run([exe, "hip", str(n), "2", "ones", "-", *ops, "dog", f"time:{calls}"], capture_output=True,
                            text=True, timeout=120)
         m = re.search(r"([0-9.]+) ms per GenerateDoG", r.stderr)
         out[key] = float(m.group(1)) if (r.returncode == 0 and m) else None
+    pyr = 4 * 5 * pyramid_pixels(n, n, octaves_for(n))  # bytes each way per call
     if out.get("mirror_host_ms"):
-        pyr = 4 * 5 * pyramid_pixels(n, n, octaves_for(n))  # bytes each way per call
-        out["pcie_GBps_each_way"] = round(pyr / (out["mirror_host_ms"] / 1e3) / 1e9, 1)
+        out["pcie_GBps_d2h"] = round(pyr / (out["mirror_host_ms"] / 1e3) / 1e9, 1)
+    if out.get("mirror_untracked_ms"):
+        out["pcie_GBps_each_way_untracked"] = round(pyr / (out["mirror_untracked_ms"] / 1e3) / 1e9, 1)
     return out
 
 
@@ -452,7 +456,9 @@ def gpu_state(pci):
     import subprocess
 
     smi = shutil.which("rocm-smi") or ("/opt/rocm/bin/rocm-smi" if os.path.exists("/opt/rocm/bin/rocm-smi") else None)
-    if not smi:
+    if not smi or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        # under rocprofv3 the child inherits the profiler's preload, which initialises the GPU
+        # before rocm-smi's `#!/usr/bin/env python3` re-execs: skip the informational query
         return None
     try:
         r = subprocess.run([smi, "--showclocks", "--showpower", "--showtemp", "--showbus", "--json"],

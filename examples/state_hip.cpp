@@ -11,6 +11,8 @@
 //   reseat:O:S:R                                point GaussPy[O][S][R] at a fresh copy of the row
 //   mirror:0|1  dirty  syncdev  synchost        mirror_host, host_dirty = true, SyncDevice, SyncHost
 //   time:CALLS                                  time CALLS back-to-back GenerateDoG calls (stderr)
+//   track:0|1                                   TrackWrites (write-tracked mirror, default on)
+//   written                                     print `written=<bytes>` (the next upload) to stderr
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -60,6 +62,8 @@ static int run(G& g, int n, int S, const char* path, int nops, char** ops, int a
         else if (op == "dirty") g.host_dirty = true;
         else if (op == "syncdev") g.SyncDevice();
         else if (op == "synchost") g.SyncHost();
+        else if (op == "track") g.TrackWrites(num(1) != 0);
+        else if (op == "written") std::fprintf(stderr, "written=%lld\n", g.written_bytes());
         else if (op == "zero" || op == "neg" || op == "scale" || op == "set" || op == "reseat") {
             const int o = num(1), s = num(2), len = n >> o;
             if (op == "zero" || op == "neg") {

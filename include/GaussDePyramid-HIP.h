@@ -24,9 +24,15 @@
 //    GenerateDoG_mpi) the host GaussPy is uploaded to the device, and after it the device pyramid
 //    is copied back into GaussPy; GaussPyInit re-reads `data` (:80).  A caller may write
 //    g.GaussPy[o][s][r][c] (or g.data[r][c]) at any time and the next call processes the edit.
-//    Cost: one pyramid H2D + one D2H per call (PCIe; 447 MB each way at 4096^2);
-//    GenerateDoG / GenerateDoG_mpi overlap the two directions and the kernel over row chunks
-//    (gdp_generate_dog_mirrored) while the rows still point into the pinned mirror.
+//    Cost: the upload is only of what the caller wrote.  The pinned mirror is write-protected
+//    whenever it equals the device copy (gdp_host_track / gdp_host_arm); a CPU write to a page
+//    faults once and is recorded, and the next mutating call uploads only the written pages
+//    (gdp_upload_image_written, gdp_generate_dog_mirrored_written) — none in main.cpp's loop
+//    (:66-73), which never writes GaussPy.  The D2H copy back is one per call (447 MB at 4096^2,
+//    INTEGRATION §2c); GenerateDoG / GenerateDoG_mpi overlap it with the kernel over row chunks.
+//    Writes that do not fault on the CPU (read(2) into GaussPy — EFAULT on a protected page —, or
+//    DMA into it) are not seen: call TrackWrites(false) first, and every call uploads the whole
+//    mirror as before (also the fallback when page protection is unavailable).
 //  - mirror_host = false: the device pyramid is the state; GaussPy is refreshed only by
 //    SyncHost(), and host edits reach the device only through SyncDevice() — or set
 //    `host_dirty = true` after editing and the next mutating call uploads first (then clears it).
@@ -76,6 +82,16 @@ public:
     bool host_dirty;   // mirror_host == false: the caller edited GaussPy / data; the next call uploads first
     void SyncHost();   // copy the device pyramid into GaussPy now
     void SyncDevice(); // copy GaussPy (the host pyramid, possibly edited) into the device pyramid now
+    // Write tracking of the mirror (default on when pinned memory and page protection are
+    // available): off, every mutating call uploads the whole mirror (see the header comment).
+    void TrackWrites(bool on);
+    bool tracking_writes() const { return track_; }
+    // Bytes of GaussPy in pages written since the mirror was last armed (the next call's upload),
+    // or -1 when no such record exists (not tracked / not armed: the next call uploads everything).
+    long long written_bytes() const {
+        size_t b = 0;
+        return track_ && armed_ && gdp_host_written_bytes(host_, &b) == GDP_OK ? (long long)b : -1;
+    }
     gdp_ctx* context() const { return ctx_; }
 
 protected:
@@ -87,6 +103,9 @@ protected:
     bool fresh_;  // contents == GaussPyInit(): GenerateDoG may use the fused build kernel
     float* host_; // pinned host pyramid in the device layout that the GaussPy rows point into
                   // (gdp_host_alloc); NULL: rows are separate new[] arrays (pinned memory refused)
+    bool track_;  // host_ is write-tracked (gdp_host_track)
+    bool armed_;  // the device pyramid equals host_ as of its last arming and the pages written
+                  // since are recorded: the next mutating call may upload only those
     bool rows_in_mirror_() const {  // every GaussPy row still where the constructor put it
         if (!host_) return false;
         for (int o = 0; o < layer; ++o)
@@ -99,7 +118,44 @@ protected:
         return true;
     }
     void pull_host_() {  // before a mutating call: the caller's GaussPy is the state
-        if (mirror_host || host_dirty) SyncDevice();
+        const bool clean = armed_;
+        armed_ = false;  // the call changes the device; SyncHost re-arms
+        if (!(mirror_host || host_dirty)) return;
+        if (clean && rows_in_mirror_())
+            check_(ctx_, gdp_upload_image_written(ctx_, 0, host_), "SyncDevice");
+        else
+            upload_();
+        host_dirty = false;
+        fresh_ = false;  // the contents are the caller's now, not necessarily GaussPyInit's
+    }
+    void upload_() {  // the whole mirror: one H2D DMA copy, or staged row gathers
+        check_(ctx_, rows_in_mirror_() ? gdp_upload_image_raw(ctx_, 0, host_)
+                                       : gdp_upload_pyramid_rows(ctx_, 0, (const float* const* const* const*)GaussPy),
+               "SyncDevice");
+    }
+    void arm_() {  // host_ == the device copy now: protect it again (or stop tracking if refused)
+        armed_ = false;
+        if (!track_ || !rows_in_mirror_()) return;
+        if (gdp_host_arm(host_) == GDP_OK) {
+            armed_ = true;
+        } else {
+            (void)gdp_host_untrack(host_);
+            track_ = false;
+        }
+    }
+    int mirrored_call_() {  // gdp_generate_dog_mirrored(_written) on host_, the status returned
+        const bool clean = armed_;
+        armed_ = false;
+        return clean ? gdp_generate_dog_mirrored_written(ctx_, 0, host_) : gdp_generate_dog_mirrored(ctx_, 0, host_);
+    }
+    void mirrored_done_() {  // after a successful mirrored call: host_ == the device copy
+        host_dirty = false;
+        fresh_ = false;
+        arm_();
+    }
+    void mirrored_(const char* what) {
+        check_(ctx_, mirrored_call_(), what);
+        mirrored_done_();
     }
     static void check_(gdp_ctx* c, int status, const char* what) {
         if (status != GDP_OK) {
@@ -112,11 +168,11 @@ protected:
 
 inline GaussPyramid_hip::GaussPyramid_hip()
     : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), host_dirty(false), length(0), S(0),
-      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {}
+      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr), track_(false), armed_(false) {}
 
 inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device)
     : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), host_dirty(false), length(len), S(S_),
-      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr) {
+      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr), track_(false), armed_(false) {
     data = new int*[len];
     for (int i = 0; i < len; ++i) {
         data[i] = new int[len];
@@ -131,6 +187,7 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
     // rate; if pinned memory is refused, separate rows and the staged scatter are used instead.
     void* h = nullptr;
     if (gdp_host_alloc(gdp_image_floats(ctx_) * sizeof(float), &h) == GDP_OK) host_ = static_cast<float*>(h);
+    track_ = host_ && gdp_host_track(host_, gdp_image_floats(ctx_) * sizeof(float)) == GDP_OK;
     GaussPy = new float***[layer];
     for (int o = 0; o < layer; ++o) {
         const int n = len >> o;
@@ -150,17 +207,28 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
 inline void GaussPyramid_hip::SyncHost() {  // one DMA copy (pinned mirror) or one staged copy per 64 MiB
     check_(ctx_, rows_in_mirror_() ? gdp_download_image_raw(ctx_, 0, host_) : gdp_download_pyramid_rows(ctx_, 0, GaussPy),
            "SyncHost");
+    arm_();
 }
 
-inline void GaussPyramid_hip::SyncDevice() {  // the inverse: one H2D DMA copy, or staged row gathers
-    check_(ctx_, rows_in_mirror_() ? gdp_upload_image_raw(ctx_, 0, host_)
-                                   : gdp_upload_pyramid_rows(ctx_, 0, (const float* const* const* const*)GaussPy),
-           "SyncDevice");
+inline void GaussPyramid_hip::SyncDevice() {  // the inverse: the whole mirror, one H2D DMA copy or staged row gathers
+    upload_();
     host_dirty = false;
     fresh_ = false;  // the contents are the caller's now, not necessarily GaussPyInit's
+    arm_();
+}
+
+inline void GaussPyramid_hip::TrackWrites(bool on) {
+    if (!on && track_) {
+        check_(ctx_, gdp_host_untrack(host_), "TrackWrites");  // every page writable again
+        track_ = armed_ = false;
+    } else if (on && !track_ && host_) {
+        // armed by the next SyncHost (every mutating call with mirror_host ends in one)
+        track_ = gdp_host_track(host_, gdp_image_floats(ctx_) * sizeof(float)) == GDP_OK;
+    }
 }
 
 inline void GaussPyramid_hip::GaussPyInit() {  // :60-87, from the CURRENT `data` (:80)
+    armed_ = false;  // every level is refilled on the device
     if (mirror_host || host_dirty)
         check_(ctx_, gdp_set_input_rows(ctx_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
     host_dirty = false;  // every level is refilled: host edits of GaussPy are overwritten, as in :76-86
@@ -179,11 +247,10 @@ inline void GaussPyramid_hip::GaussFilter(int theLayer) {
 
 inline void GaussPyramid_hip::GenerateDoG() {
     if (mirror_host && rows_in_mirror_()) {
-        // GaussPy mirrored in the pinned device-layout buffer: upload, in-place pass and download
-        // in one call, pipelined over row chunks (both PCIe directions and the kernel overlap)
-        check_(ctx_, gdp_generate_dog_mirrored(ctx_, 0, host_), "GenerateDoG");
-        host_dirty = false;
-        fresh_ = false;
+        // GaussPy mirrored in the pinned device-layout buffer: upload (only the pages written since
+        // the last call when tracked), in-place pass and download in one call, pipelined over row
+        // chunks
+        mirrored_("GenerateDoG");
         return;
     }
     // on freshly initialised contents the fused single-pass build is bit-identical to
@@ -202,11 +269,10 @@ inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
     if (!piped) pull_host_();
     check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi");
     if (piped) {
-        const int rc = gdp_generate_dog_mirrored(ctx_, 0, host_);
+        const int rc = mirrored_call_();
         check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_SERIAL), "GenerateDoG_mpi");
         check_(ctx_, rc, "GenerateDoG_mpi");
-        host_dirty = false;
-        fresh_ = false;
+        mirrored_done_();
         return;
     }
     const int rc = fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr);
@@ -242,6 +308,7 @@ inline GaussPyramid_hip::~GaussPyramid_hip() {
         }
         delete[] GaussPy;
     }
+    if (track_) (void)gdp_host_untrack(host_);
     gdp_host_free(host_);
     if (data) {
         for (int i = 0; i < length; ++i) delete[] data[i];

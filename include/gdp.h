@@ -258,9 +258,35 @@ int gdp_download_image_raw(gdp_ctx* ctx, int b, float* host);
  * bit-identical to gdp_upload_image_raw(b, host) + gdp_generate_dog + gdp_download_image_raw(b,
  * host) for that image, but pipelined over row chunks so the host-to-device copies, the kernel and
  * the device-to-host copies overlap (two copy streams beside the context's).  `host` should be
- * pinned (gdp_host_alloc) for the copies to be asynchronous.  Blocking.  This is what the C++
- * drop-ins run for GenerateDoG() when GaussPy is mirrored (mirror_host, the default). */
+ * pinned (gdp_host_alloc) for the copies to be asynchronous.  Blocking.  The overlap is
+ * best-effort: the two copy streams share the process's hardware queues (4 on the MI355X boxes)
+ * with every other stream and context, so under concurrent work the copies may serialise with
+ * the kernel — the result is the same either way.  This is what the C++ drop-ins run for
+ * GenerateDoG() when GaussPy is mirrored (mirror_host, the default) and not write-tracked. */
 int gdp_generate_dog_mirrored(gdp_ctx* ctx, int b, float* host);
+
+/* ---- write-tracked host mirrors (GuassDePyramid.h:16's two-way GaussPy, main.cpp:66-73) ------
+ * A mirror that the caller usually does not write (main.cpp's loop never writes GaussPy) need not
+ * be uploaded before every call.  gdp_host_track registers a host buffer (gdp_host_alloc memory,
+ * or any page-aligned anonymous memory) and installs a SIGSEGV handler (once per process; faults
+ * elsewhere go to the handler installed before it, or take the default action).  gdp_host_arm
+ * write-protects the buffer's pages — the caller asserts that the buffer now equals the device
+ * copy it mirrors; the first CPU write to each page then faults once, is recorded, and the page is
+ * writable again.  gdp_upload_image_written / gdp_generate_dog_mirrored_written are
+ * gdp_upload_image_raw / gdp_generate_dog_mirrored that upload only the pages written since the
+ * buffer was armed (the caller asserts image b's device pyramid equals the buffer as of arming),
+ * and re-arm it; on a buffer that is not tracked or not armed they upload everything (and arm it
+ * if tracked).  gdp_host_written_bytes: bytes of the buffer in pages written since arming
+ * (GDP_ERR_STATE when not armed).  gdp_host_untrack makes every page writable and forgets it.
+ * Not seen (untrack such buffers): writes that do not fault on the CPU — DMA into the buffer, or
+ * a system call such as read(2), which fails with EFAULT on a protected page.  GDP_ERR_STATE from
+ * gdp_host_track: page protection is unavailable for this memory or no slot is free (64). */
+int gdp_host_track(void* host, size_t bytes);
+int gdp_host_untrack(void* host);
+int gdp_host_arm(void* host);
+int gdp_host_written_bytes(const void* host, size_t* bytes);
+int gdp_upload_image_written(gdp_ctx* ctx, int b, const float* host);
+int gdp_generate_dog_mirrored_written(gdp_ctx* ctx, int b, float* host);
 /* Order-independent 64-bit checksum of image b's pyramid (blocking): the sum, mod 2^64, over
  * every word of every level of splitmix64_fin(idx * 0x9E3779B97F4A7C15 + (o*64+s) *
  * 0xD1B54A32D192ED03 + float_bits), idx = global_row * cols + col.  Row-band checksums add up

@@ -99,6 +99,12 @@ SIGNATURES = {
     "gdp_image_floats": (_c_size, [_p]),
     "gdp_download_image_raw": (_c_int, [_p, _c_int, _p]),
     "gdp_generate_dog_mirrored": (_c_int, [_p, _c_int, _p]),
+    "gdp_host_track": (_c_int, [_p, _c_size]),
+    "gdp_host_untrack": (_c_int, [_p]),
+    "gdp_host_arm": (_c_int, [_p]),
+    "gdp_host_written_bytes": (_c_int, [_p, ctypes.POINTER(ctypes.c_size_t)]),
+    "gdp_upload_image_written": (_c_int, [_p, _c_int, _p]),
+    "gdp_generate_dog_mirrored_written": (_c_int, [_p, _c_int, _p]),
     "gdp_checksum": (_c_int, [_p, _c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "gdp_get_taps": (_c_int, [_p, _c_int, _c_int, _c_int, _p]),
     "gdp_set_window_centre": (_c_int, [_p, _c_int]),

@@ -30,7 +30,13 @@
 #include <type_traits>
 #include <utility>
 #include <array>
+#include <atomic>
+#include <mutex>
 #include <vector>
+
+#include <signal.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include "gdp.h"
 
@@ -43,6 +49,7 @@ namespace {
 #include "gdp_inplace.inc"
 #include "gdp_conv.inc"
 #include "gdp_util.inc"
+#include "gdp_track.inc"
 
 // ------------------------------------------------------------------------------------------
 // host side
@@ -513,28 +520,10 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
 
 template <int L, int T, int W>
 hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
-    auto k = k_conv_blk<L, T, W, kBkHaloLanes>;
-#ifdef GDP_EXPERIMENTS
-    // research A/B (S = 2 only): rows unrolled together x exact waves per SIMD (k_conv_blk_x)
-    if constexpr (L == 5 && T / W >= 2) {
-        static const int ur = [] { const char* e = std::getenv("GDP_CONV_UNROLL"); return e ? std::atoi(e) : 0; }();
-        static const int wv = [] { const char* e = std::getenv("GDP_CONV_WAVES_PER_SIMD"); return e ? std::atoi(e) : 8; }();
-        if (ur > 0) {
-            const int key = ur * 10 + wv;
-            switch (key) {
-                case 18: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 1, 8>; break;
-                case 16: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 1, 6>; break;
-                case 28: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 2, 8>; break;
-                case 26: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 2, 6>; break;
-                case 24: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 2, 4>; break;
-                case 38: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 3, 8>; break;
-                case 36: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 3, 6>; break;
-                case 34: k = k_conv_blk_x<L, T, W, kBkHaloLanes, 3, 4>; break;
-                default: return hipErrorInvalidConfiguration;
-            }
-        }
-    }
-#endif
+    // the default pacing (vmcnt(2)) compiled in for the 16-wave tiles; any other pace, and the
+    // 8-wave tiles, read it at run time
+    auto k = (W == 16 && c->geom.conv_pace == 2) ? k_conv_blk<L, T, W, kBkHaloLanes, 2>
+                                                 : k_conv_blk<L, T, W, kBkHaloLanes, kPaceRuntime>;
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64 * W), 0, st, c->d_geom, c->d_in, c->d_out, units, c->conv_order,
                        c->d_conv_perm);
@@ -1405,6 +1394,9 @@ int gdp_build_gaussian(gdp_ctx* c, void* stream) try {
     // 0) for S = 0..3; both take the octaves whose width is a multiple of 4, the LDS tiles the rest
     // (and everything for other S or conv_kernel = 1)
     const bool sweep = c->conv_kernel != 1 && g.L >= 3 && g.L <= (c->conv_kernel == 2 ? 8 : 6);
+    // the block tiles address a wave's rows as byte offsets from its first row (k_conv_blk)
+    if (sweep && c->conv_kernel == 2 && 65ll * 4 * g.W >= kOOB)
+        return c->status(GDP_ERR_ARG, "gdp_build_gaussian: width %d too large for the block tiles", g.W);
     {  // rows per tile / strip (and waves per block) the selected kernel is instantiated for
         const int r = c->conv_rows, k = c->conv_kernel, w = c->conv_waves;
         if (sweep && k == 0 && r != 16 && r != 32)
@@ -1874,9 +1866,9 @@ int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
 // both directions and the kernel overlap: chunk j's upload (copy stream 1) runs beside chunk j-1's
 // pass (the context's stream) and chunk j-2's download (copy stream 2).  The op is pointwise in
 // (octave, row, column) across the S+3 levels, so any row split is exact.
-int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
-    if (!c || !host || b < 0 || b >= c->geom.batch)
-        return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored: bad argument") : GDP_ERR_ARG;
+// `runs` (write-tracked mirrors): instead of every chunk, upload only these byte ranges of the
+// image (the pages written since the mirror was armed), all before the first chunk's pass.
+static int generate_dog_mirrored(gdp_ctx* c, int b, float* host, const std::vector<std::pair<size_t, size_t>>* runs) {
     const Geom& g = c->geom;
     GDP_HIP(c, hipSetDevice(c->device));
     if (!c->st_up) GDP_HIP(c, hipStreamCreateWithFlags(&c->st_up, hipStreamNonBlocking));
@@ -1921,11 +1913,17 @@ int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
     GDP_HIP(c, hipEventRecord(ev[2 * chunks.size()], c->stream));
     GDP_HIP(c, hipStreamWaitEvent(c->st_up, ev[2 * chunks.size()], 0));
     auto image_level = [&](int o, int s) { return g.oct[o].lev_off + (long long)s * g.oct[o].lev_stride; };
+    if (runs) {
+        char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * g.pyr_stride);
+        for (const auto& r : *runs)
+            GDP_HIP(c, hipMemcpyAsync(dev + r.first, reinterpret_cast<const char*>(host) + r.first, r.second - r.first,
+                                      hipMemcpyHostToDevice, c->st_up));
+    }
     for (size_t j = 0; j < chunks.size(); ++j) {
         const Chunk& ch = chunks[j];
         const OctGeom& og = g.oct[ch.o];
         const size_t off = (size_t)ch.r0 * og.cols, n = (size_t)(ch.r1 - ch.r0) * og.cols;
-        for (int s = 0; s < g.L; ++s)
+        for (int s = 0; s < g.L && !runs; ++s)
             GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, ch.o, s)) + off,
                                       host + image_level(ch.o, s) + off, n * 4, hipMemcpyHostToDevice, c->st_up));
         GDP_HIP(c, hipEventRecord(ev[2 * j], c->st_up));
@@ -1945,6 +1943,150 @@ int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
     GDP_HIP(c, hipStreamSynchronize(c->st_down));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     drain.armed = false;
+    return GDP_OK;
+}
+
+int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored: bad argument") : GDP_ERR_ARG;
+    return generate_dog_mirrored(c, b, host, nullptr);
+} GDP_ABI_CATCH(c)
+
+// ---- write-tracked host mirrors (gdp_track.inc) ----
+int gdp_host_track(void* host, size_t bytes) try {
+    if (!host || bytes == 0) return GDP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    if (track_find(host)) return GDP_OK;
+    if (!g_segv_installed) {
+        const long pg = sysconf(_SC_PAGESIZE);
+        if (pg > 0) g_page_bytes = (size_t)pg;
+        struct sigaction sa;
+        std::memset(&sa, 0, sizeof sa);
+        sa.sa_sigaction = track_on_segv;
+        sa.sa_flags = SA_SIGINFO | SA_RESTART | SA_ONSTACK;
+        sigemptyset(&sa.sa_mask);
+        if (sigaction(SIGSEGV, &sa, &g_prev_segv) != 0) return GDP_ERR_STATE;
+        g_segv_installed = true;
+    }
+    TrackedMirror* t = nullptr;
+    for (TrackedMirror& s : g_tracked)
+        if (!s.base.load(std::memory_order_relaxed)) {
+            t = &s;
+            break;
+        }
+    if (!t) return GDP_ERR_STATE;
+    const uintptr_t u = reinterpret_cast<uintptr_t>(host);
+    const uintptr_t base = u / g_page_bytes * g_page_bytes;
+    const uintptr_t end = (u + bytes + g_page_bytes - 1) / g_page_bytes * g_page_bytes;
+    // protection must be available on this memory (a probe of its first page)
+    if (mprotect(reinterpret_cast<void*>(base), g_page_bytes, PROT_READ) != 0) return GDP_ERR_STATE;
+    if (mprotect(reinterpret_cast<void*>(base), g_page_bytes, PROT_READ | PROT_WRITE) != 0) return GDP_ERR_STATE;
+    t->pages = (end - base) / g_page_bytes;
+    t->written = new std::atomic<unsigned char>[t->pages];
+    for (size_t p = 0; p < t->pages; ++p) t->written[p].store(0, std::memory_order_relaxed);
+    t->user = host;
+    t->user_bytes = bytes;
+    t->armed = false;
+    t->bytes.store(end - base, std::memory_order_relaxed);
+    t->base.store(base, std::memory_order_release);
+    return GDP_OK;
+} GDP_ABI_CATCH(nullptr)
+
+int gdp_host_untrack(void* host) try {
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    TrackedMirror* t = host ? track_find(host) : nullptr;
+    if (!t) return GDP_ERR_ARG;
+    const uintptr_t base = t->base.load(std::memory_order_relaxed);
+    const int rc = mprotect(reinterpret_cast<void*>(base), t->bytes.load(std::memory_order_relaxed), PROT_READ | PROT_WRITE) == 0
+                       ? GDP_OK
+                       : GDP_ERR_STATE;
+    t->base.store(0, std::memory_order_release);
+    t->bytes.store(0, std::memory_order_relaxed);
+    delete[] t->written;
+    t->written = nullptr;
+    t->user = nullptr;
+    t->armed = false;
+    return rc;
+} GDP_ABI_CATCH(nullptr)
+
+int gdp_host_arm(void* host) try {
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    TrackedMirror* t = host ? track_find(host) : nullptr;
+    if (!t) return GDP_ERR_ARG;
+    return track_rearm(*t, {}, true);
+} GDP_ABI_CATCH(nullptr)
+
+int gdp_host_written_bytes(const void* host, size_t* bytes) try {
+    if (!bytes) return GDP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    const TrackedMirror* t = host ? track_find(host) : nullptr;
+    if (!t) return GDP_ERR_ARG;
+    if (!t->armed) return GDP_ERR_STATE;
+    const uintptr_t b = t->base.load(std::memory_order_relaxed);
+    const uintptr_t u0 = reinterpret_cast<uintptr_t>(t->user), u1 = u0 + t->user_bytes;
+    size_t n = 0;
+    for (size_t p = 0; p < t->pages; ++p)
+        if (t->written[p].load(std::memory_order_relaxed)) {
+            const uintptr_t lo = std::max<uintptr_t>(u0, b + p * g_page_bytes);
+            const uintptr_t hi = std::min<uintptr_t>(u1, b + (p + 1) * g_page_bytes);
+            n += hi > lo ? hi - lo : 0;
+        }
+    *bytes = n;
+    return GDP_OK;
+} GDP_ABI_CATCH(nullptr)
+
+// The written pages of an armed mirror covering image b, or nullptr when the whole image must be
+// uploaded (not tracked / not armed / smaller than the image / too fragmented).  Caller holds
+// g_track_mu.
+static TrackedMirror* track_for_image(const gdp_ctx* c, const void* host, std::vector<std::pair<size_t, size_t>>* runs) {
+    TrackedMirror* t = track_find(host);
+    if (!t) return nullptr;
+    const size_t img_bytes = (size_t)c->img_floats * 4;
+    if (!t->armed || t->user_bytes < img_bytes) return t;
+    *runs = track_written_runs(*t);
+    for (auto& r : *runs) r.second = std::min(r.second, img_bytes);
+    runs->erase(std::remove_if(runs->begin(), runs->end(), [](const std::pair<size_t, size_t>& r) { return r.second <= r.first; }),
+                runs->end());
+    return t;
+}
+
+int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_written: bad argument") : GDP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    std::vector<std::pair<size_t, size_t>> runs;
+    TrackedMirror* t = track_for_image(c, host, &runs);
+    const bool partial = t && t->armed && t->user_bytes >= (size_t)c->img_floats * 4 && runs.size() <= 4096;
+    GDP_HIP(c, hipSetDevice(c->device));
+    if (partial) {
+        char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
+        for (const auto& r : runs)
+            GDP_HIP(c, hipMemcpyAsync(dev + r.first, reinterpret_cast<const char*>(host) + r.first, r.second - r.first,
+                                      hipMemcpyHostToDevice, c->stream));
+    } else {
+        GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, host, (size_t)c->img_floats * 4,
+                                  hipMemcpyHostToDevice, c->stream));
+    }
+    GDP_HIP(c, hipStreamSynchronize(c->stream));
+    if (t && track_rearm(*t, runs, !partial) != GDP_OK)
+        return c->status(GDP_ERR_STATE, "gdp_upload_image_written: mprotect refused re-arming the mirror");
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+int gdp_generate_dog_mirrored_written(gdp_ctx* c, int b, float* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored_written: bad argument") : GDP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    std::vector<std::pair<size_t, size_t>> runs;
+    TrackedMirror* t = track_for_image(c, host, &runs);
+    const bool partial = t && t->armed && t->user_bytes >= (size_t)c->img_floats * 4 && runs.size() <= 4096;
+    const int rc = generate_dog_mirrored(c, b, host, partial ? &runs : nullptr);
+    if (rc != GDP_OK) {
+        if (t) t->armed = false;  // the device may hold a partial result: the next call uploads all
+        return rc;
+    }
+    if (t && track_rearm(*t, runs, !partial) != GDP_OK)
+        return c->status(GDP_ERR_STATE, "gdp_generate_dog_mirrored_written: mprotect refused re-arming the mirror");
     return GDP_OK;
 } GDP_ABI_CATCH(c)
 

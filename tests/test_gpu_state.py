@@ -9,6 +9,7 @@ bit-identical (0 ULP) to the oracle's in-place restatement (gauss_octave / gener
 GenerateDoG_nomp_dynamic's subset) applied to the same edited pyramid.  Runs on an MI355X.
 """
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -89,8 +90,8 @@ class _Replay:
             self.host[:] = self.pyr
         elif f[0] == "data":
             self.img[int(f[1]), int(f[2])] = int(f[3])
-        elif f[0] == "reseat":
-            pass  # same contents, another address
+        elif f[0] in ("reseat", "track", "written"):
+            pass  # same contents, another address / the upload strategy / a report
         else:
             lv = self._lv(self.host, int(f[1]), int(f[2]))
             if f[0] == "zero":
@@ -118,11 +119,13 @@ def _run(oracle, tmp_path, cls, n, S, spec, ops):
     if not os.path.exists(EXE):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
     out = tmp_path / "state.f32"
-    subprocess.run([EXE, cls, str(n), str(S), spec, str(out), *ops], check=True, timeout=120)
+    r = subprocess.run([EXE, cls, str(n), str(S), spec, str(out), *ops], check=True, timeout=120, capture_output=True,
+                       text=True)
     rp = _Replay(oracle, cls, n, S, spec)
     for op in ops:
         rp.apply(op)
     _assert_same(np.fromfile(out, dtype=np.float32), rp.host, (cls, n, S, ops))
+    return [int(x) for x in re.findall(r"written=(-?\d+)", r.stderr)]
 
 
 EDITS = ["zero:0:1", "scale:0:2:5:-3.5", "neg:1:0", "set:0:0:3:7:-1e30", "set:2:3:1:1:3.0e38"]
@@ -136,6 +139,33 @@ def test_cpp_class_processes_host_edits(oracle, tmp_path, n, S):
     _run(oracle, tmp_path, "hip", n, S, "lcg:4", ["dog"] + EDITS + ["dog", "scale:1:1:0:0.25", "mpi"])
     _run(oracle, tmp_path, "hip", n, S, "lcg:5", EDITS + ["init", "dog"])  # refill overwrites the edits
     _run(oracle, tmp_path, "hip", n, S, "lcg:6", ["data:3:5:-70000", "data:0:0:2147483647", "init", "zero:0:4", "dog"])
+
+
+def test_cpp_class_write_tracked_mirror_uploads_what_was_written(oracle, tmp_path):
+    """the default mirror is write-tracked (gdp_host_track) — after each call
+    it is write-protected, a CPU write faults once and is recorded, and the next call uploads only
+    the written pages.  A single float written after a call (after SyncHost) is processed; a call
+    with nothing written uploads nothing; edits spanning levels, GaussPyInit, GaussFilter, the MPI
+    entry, TrackWrites(false / true) and mirror_host toggles all stay bit-identical to the oracle."""
+    page = os.sysconf("SC_PAGESIZE")
+    n, S = 64, 2
+    w = _run(oracle, tmp_path, "hip", n, S, "lcg:13", ["written", "dog", "written", "set:0:0:3:7:-1e30", "written",
+                                                        "dog", "written", "dog", "written"])
+    assert w == [0, 0, page, 0, 0], w
+    w = _run(oracle, tmp_path, "hip", n, S, "lcg:14", ["dog", "synchost", "set:2:4:1:1:5.5", "written", "filter:2",
+                                                        "written", "zero:0:1", "neg:1:3", "mpi", "written"])
+    assert w[0] == page and w[1] == 0 and w[2] == 0, w
+    w = _run(oracle, tmp_path, "hip", 100, S, "lcg:15", ["track:0", "written", "set:0:0:3:7:1e20", "dog", "track:1",
+                                                         "written", "neg:0:0", "dog", "written", "scale:1:1:2:-2",
+                                                         "written", "dog"])
+    assert w[0] == -1 and w[1] == -1 and w[2] == 0 and w[3] > 0, w  # untracked: whole uploads
+    w = _run(oracle, tmp_path, "hip", n, S, "lcg:16", ["dog", "mirror:0", "set:0:0:0:0:9", "dog", "mirror:1", "written",
+                                                       "neg:0:2", "dog", "written"])
+    assert w == [-1, 0], w  # a call without the mirror disarms: the next mirrored call uploads all
+    w = _run(oracle, tmp_path, "a512xp", n, S, "lcg:17", ["dog", "set:0:1:2:2:-4", "written", "filter:0", "dog"])
+    assert w == [page], w
+    w = _run(oracle, tmp_path, "hip", n, S, "lcg:18", EDITS + ["init", "written", "set:0:0:3:7:2", "dog", "dog"])
+    assert w == [0], w
 
 
 def test_cpp_class_without_mirror_uploads_only_when_told(oracle, tmp_path):
