@@ -893,9 +893,10 @@ def main():
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip gdp_autotune (by default the build kernel variant is chosen by timing every "
                          "variant on this device before the warm-up; all variants give identical bits)")
-    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4, 8, 16],
+    ap.add_argument("--inplace-sub", type=int, default=None, choices=[0, 1, 2, 4, 8, 16, -16],
                     help="--op regen/gauss: force the in-place block shape (GDP_TUNE_INPLACE_SUB / _WINDOW_SUB: "
-                         "1024 / N threads, 0 = k_levels_x) and skip its autotune, e.g. for profiling runs")
+                         "1024 / N threads, 0 = k_levels_x, -16 = 16 x 256 block tiles) and skip its autotune, e.g. "
+                         "for profiling runs")
     ap.add_argument("--input", default="i32", choices=["i32", "u8"],
                     help="input pixel format (i32 = the reference's int image; u8 = 8-bit images)")
     ap.add_argument("--op", default="build", choices=["build", "regen", "gauss", "conv", "subset"],
@@ -915,7 +916,8 @@ def main():
                          "8 waves: 8 / 16 / 24 / 32 rows)")
     ap.add_argument("--conv-order", type=int, default=None,
                     help="--op conv: block order bits (1 XCD-chunked, 2 alternate sweep directions, 4 octave rows "
-                         "after their input rows; default 4)")
+                         "after their input rows; default 5, and 4 for one image of >= 2^27 pixels — gdp.h "
+                         "GDP_TUNE_CONV_ORDER)")
     ap.add_argument("--scatter", action="store_true",
                     help="N > 1: also measure the input split (rank 0's image batch, or for the row-band config its "
                          "image's rows, scattered over RCCL, SURVEY.md §8e), outside the timed region, and check the "
@@ -1068,7 +1070,7 @@ def main():
             c.build(stream)  # materialise the pyramid the in-place passes work on
         steps_fn = [c.generate_dog if args.op == "regen" else (lambda st, c=c: c.gauss_range(0, O, st))
                     for c in ctxs]
-        key, values = (("inplace_sub", [1, 4, 2, 0, 8, 16]) if args.op == "regen" else
+        key, values = (("inplace_sub", [1, 4, 2, 0, 8, 16, -16]) if args.op == "regen" else
                        ("window_sub", [1, 4, 2, 8, 16]))
         if args.inplace_sub is not None:
             if args.inplace_sub not in values:
@@ -1210,6 +1212,8 @@ def main():
                                                                      "vmcnt(%d)" % tun["store_pace"])
                        if args.op == "subset" else
                        {"regen": ("k_levels_x (in-place window+DoG, one level per wave)" if tun["inplace_sub"] == 0 else
+                                  "k_levels_tile<MODE=3> (in-place window+DoG, all octaves, 16-row x 256-column block "
+                                  "tiles of k_build's shape)" if tun["inplace_sub"] < 0 else
                                   "k_levels<MODE=3> (in-place window+DoG, all octaves, %d-thread blocks)"
                                   % (1024 // tun["inplace_sub"])) + ", zero window %d, store pace %s" % (
                                      tun["zero_window"], "off" if tun["inplace_pace"] < 0 else "vmcnt(%d)" % tun["inplace_pace"])

@@ -89,6 +89,11 @@ public:
     enum { ROLES_AUTO = 0, ROLES_BANDS = 1, ROLES_REFERENCE = 2 };
     int roles = ROLES_BANDS;  // see the header comment; decided at the first GenerateDoG_mpi
     int collector() const { return ref_roles_ ? S + 3 : 0; }  // the rank holding the pyramid
+    // The role map a world of `world` ranks runs under `roles` (ROLES_AUTO: the reference's from
+    // S+4 ranks on) — what the first GenerateDoG_mpi decides; read the pyramid on collector().
+    static bool reference_roles(int roles_, int world, int S_) {
+        return roles_ == ROLES_REFERENCE || (roles_ == ROLES_AUTO && world >= S_ + 4);
+    }
     bool mirror_host = true;  // two-way GaussPy (see the header comment)
     bool host_dirty = false;  // the caller edited GaussPy / data: upload before the next call
     void SyncHost() { sync_host_(); host_current_ = true; }
@@ -267,7 +272,7 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
                          S + 4, size_);
             std::abort();
         }
-        ref_roles_ = roles == ROLES_REFERENCE || (roles == ROLES_AUTO && size_ >= S + 4);
+        ref_roles_ = reference_roles(roles, size_, S);
     }
     if (ref_roles_) {  // GaussDePyramid-MPI.h:265-335, role for role
         pull_host_();

@@ -12,9 +12,12 @@
 // GaussPy is two-way state, as in mpitest.cpp, whose GenerateDoG_* multiply and subtract the
 // GLOBAL GaussPy in place (:50-56, :89, :128-133, :165): a caller that writes GaussPy between
 // GaussPyInit(p) and GenerateDoG_mpi has that edit processed.  With `gdp_mpitest_mirror_host`
-// (default true) every GenerateDoG_* uploads GaussPy first (one H2D DMA of the pinned mirror, or
-// staged row gathers when a caller re-seated a row pointer) and runs the in-place re-entry pass on
-// it; after the call the result is copied back into GaussPy.  With it false the device pyramid is
+// (default true) every GenerateDoG_* uploads what the caller wrote into GaussPy first — the mirror
+// is write-tracked like GaussPyramid_hip's (gdp_host_alloc_tracked, round 6): only the pages
+// written since the last call, none when nothing was written; the whole mirror when tracking is
+// unavailable or `gdp_mpitest_track_writes` is false; staged row gathers when a caller re-seated a
+// row pointer — and runs the in-place re-entry pass on it; after the call the result is copied
+// back into GaussPy.  With it false the device pyramid is
 // the state: GaussPy is refreshed only after GaussPyInit / GenerateDoG_* / gdp_mpitest_SyncHost(),
 // and edits reach the device only with `gdp_mpitest_host_dirty = true` (the next call uploads first)
 // or gdp_mpitest_SyncDevice().  Only in that mode may a GenerateDoG_* right after GaussPyInit use
@@ -52,6 +55,11 @@ static bool gdp_mpitest_fresh = false;
 static float* gdp_mpitest_host = nullptr;  // pinned device-layout mirror the GaussPy rows point into
 bool gdp_mpitest_mirror_host = true;  // GaussPy two-way: upload before / download after every GenerateDoG_*
 bool gdp_mpitest_host_dirty = false;  // mirror off: the caller edited GaussPy, the next call uploads first
+// write tracking of the mirror; set false before GaussPyInit(p) to keep plain
+// pinned memory (e.g. when GaussPy is filled by read(2), which fails on a protected page)
+bool gdp_mpitest_track_writes = true;
+static bool gdp_mpitest_tracked = false;  // gdp_mpitest_host is gdp_host_alloc_tracked memory
+static bool gdp_mpitest_armed = false;    // ... protected since it last equalled the device copy
 
 static inline void gdp_mpitest_check(int status, const char* what) {
     if (status != GDP_OK) {
@@ -74,9 +82,16 @@ static inline bool gdp_mpitest_rows_in_mirror() {
     return true;
 }
 
+// GaussPy == the device copy now: write-protect the tracked mirror again
+static inline void gdp_mpitest_arm() {
+    gdp_mpitest_armed = gdp_mpitest_tracked && gdp_mpitest_rows_in_mirror() && gdp_host_arm(gdp_mpitest_host) == GDP_OK;
+}
+
 static inline int gdp_mpitest_download() {
-    return gdp_mpitest_rows_in_mirror() ? gdp_download_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
-                                        : gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy);
+    const int rc = gdp_mpitest_rows_in_mirror() ? gdp_download_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
+                                                : gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy);
+    if (rc == GDP_OK) gdp_mpitest_arm();
+    return rc;
 }
 
 // GaussPy (the host pyramid, possibly edited) -> the device pyramid now
@@ -88,6 +103,7 @@ inline void gdp_mpitest_SyncDevice() {
                       "SyncDevice");
     gdp_mpitest_host_dirty = false;
     gdp_mpitest_fresh = false;  // the caller's contents now, not necessarily GaussPyInit's
+    gdp_mpitest_arm();
 }
 
 // the device pyramid -> GaussPy now
@@ -105,8 +121,10 @@ void GaussPyInit(int* data[MAX]) {
         // the rows (one new float[] each in the reference) point into one pinned buffer in the
         // device layout: every download is a single DMA copy (separate rows if pinning is refused)
         void* h = nullptr;
-        gdp_mpitest_host = gdp_host_alloc(gdp_image_floats(gdp_mpitest_ctx) * sizeof(float), &h) == GDP_OK
-                               ? static_cast<float*>(h) : nullptr;
+        const size_t bytes = gdp_image_floats(gdp_mpitest_ctx) * sizeof(float);
+        gdp_mpitest_tracked = gdp_mpitest_track_writes && gdp_host_alloc_tracked(bytes, &h) == GDP_OK;
+        if (!gdp_mpitest_tracked && gdp_host_alloc(bytes, &h) != GDP_OK) h = nullptr;
+        gdp_mpitest_host = static_cast<float*>(h);
         GaussPy = new float***[layer];
         for (int o = 0; o < layer; ++o) {
             GaussPy[o] = new float**[S + 3];
@@ -119,6 +137,7 @@ void GaussPyInit(int* data[MAX]) {
         }
     }
     is_initialized = true;
+    gdp_mpitest_armed = false;  // every level is refilled on the device
     gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
     gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
     gdp_mpitest_host_dirty = false;  // every level refilled: host edits are overwritten, as in :462-472
@@ -131,10 +150,17 @@ static inline void gdp_mpitest_generate() {
     // the GLOBAL GaussPy is what the reference's workers multiply and its collector subtracts
     // (:128-133, :165): upload it first, then the in-place pass on exactly those contents
     if (gdp_mpitest_mirror_host && gdp_mpitest_rows_in_mirror()) {
-        // upload + in-place pass + download in one call, pipelined over row chunks
-        gdp_mpitest_check(gdp_generate_dog_mirrored(gdp_mpitest_ctx, 0, gdp_mpitest_host), "GenerateDoG_mpi");
+        // upload (the written pages only, when armed) + in-place pass + download in one call,
+        // pipelined over row chunks
+        const bool clean = gdp_mpitest_armed;
+        gdp_mpitest_armed = false;
+        gdp_mpitest_check(clean ? gdp_generate_dog_mirrored_written(gdp_mpitest_ctx, 0, gdp_mpitest_host)
+                                : gdp_generate_dog_mirrored(gdp_mpitest_ctx, 0, gdp_mpitest_host),
+                          "GenerateDoG_mpi");
+        gdp_mpitest_arm();
         gdp_mpitest_host_dirty = false;
     } else {
+        gdp_mpitest_armed = false;  // the device changes below; the download re-arms
         if (gdp_mpitest_mirror_host || gdp_mpitest_host_dirty) gdp_mpitest_SyncDevice();
         gdp_mpitest_check(gdp_mpitest_fresh ? gdp_build(gdp_mpitest_ctx, nullptr) : gdp_generate_dog(gdp_mpitest_ctx, nullptr),
                           "GenerateDoG_mpi");
@@ -163,6 +189,7 @@ void delete_mpi() {
     delete[] GaussPy;
     gdp_host_free(gdp_mpitest_host);
     gdp_mpitest_host = nullptr;
+    gdp_mpitest_tracked = gdp_mpitest_armed = false;
     gdp_destroy(gdp_mpitest_ctx);
     gdp_mpitest_ctx = nullptr;
     is_initialized = false;

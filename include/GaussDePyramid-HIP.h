@@ -24,12 +24,16 @@
 //    GenerateDoG_mpi) the host GaussPy is uploaded to the device, and after it the device pyramid
 //    is copied back into GaussPy; GaussPyInit re-reads `data` (:80).  A caller may write
 //    g.GaussPy[o][s][r][c] (or g.data[r][c]) at any time and the next call processes the edit.
-//    Cost: the upload is only of what the caller wrote.  The pinned mirror is write-protected
-//    whenever it equals the device copy (gdp_host_track / gdp_host_arm); a CPU write to a page
+//    Cost: the upload is only of what the caller wrote.  The mirror (gdp_host_alloc_tracked: the
+//    pages GaussPy points into, DMA'd through a second, registered mapping of the same memory) is
+//    write-protected whenever it equals the device copy (gdp_host_arm); a CPU write to a page
 //    faults once and is recorded, and the next mutating call uploads only the written pages
 //    (gdp_upload_image_written, gdp_generate_dog_mirrored_written) — none in main.cpp's loop
 //    (:66-73), which never writes GaussPy.  The D2H copy back is one per call (447 MB at 4096^2,
-//    INTEGRATION §2c); GenerateDoG / GenerateDoG_mpi overlap it with the kernel over row chunks.
+//    INTEGRATION §2c); GenerateDoG / GenerateDoG_mpi overlap it with the kernel over row chunks
+//    (best-effort: the copy streams share the process's hardware queues — 4 on the MI355X boxes —
+//    with every other stream and context, so under concurrent work they may serialise; the result
+//    is the same either way).
 //    Writes that do not fault on the CPU (read(2) into GaussPy — EFAULT on a protected page —, or
 //    DMA into it) are not seen: call TrackWrites(false) first, and every call uploads the whole
 //    mirror as before (also the fallback when page protection is unavailable).
@@ -186,8 +190,15 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
     // buffer laid out like the device pyramid, so SyncHost is a single DMA copy at the full PCIe
     // rate; if pinned memory is refused, separate rows and the staged scatter are used instead.
     void* h = nullptr;
-    if (gdp_host_alloc(gdp_image_floats(ctx_) * sizeof(float), &h) == GDP_OK) host_ = static_cast<float*>(h);
-    track_ = host_ && gdp_host_track(host_, gdp_image_floats(ctx_) * sizeof(float)) == GDP_OK;
+    // Write-tracked when the platform allows it (gdp_host_alloc_tracked: a registered DMA view and a
+    // protectable CPU view of the same pages), else plain pinned memory and whole uploads.
+    const size_t mirror_bytes = gdp_image_floats(ctx_) * sizeof(float);
+    if (gdp_host_alloc_tracked(mirror_bytes, &h) == GDP_OK) {
+        host_ = static_cast<float*>(h);
+        track_ = true;
+    } else if (gdp_host_alloc(mirror_bytes, &h) == GDP_OK) {
+        host_ = static_cast<float*>(h);
+    }
     GaussPy = new float***[layer];
     for (int o = 0; o < layer; ++o) {
         const int n = len >> o;
@@ -308,7 +319,6 @@ inline GaussPyramid_hip::~GaussPyramid_hip() {
         }
         delete[] GaussPy;
     }
-    if (track_) (void)gdp_host_untrack(host_);
     gdp_host_free(host_);
     if (data) {
         for (int i = 0; i < length; ++i) delete[] data[i];

@@ -267,20 +267,31 @@ int gdp_generate_dog_mirrored(gdp_ctx* ctx, int b, float* host);
 
 /* ---- write-tracked host mirrors (GuassDePyramid.h:16's two-way GaussPy, main.cpp:66-73) ------
  * A mirror that the caller usually does not write (main.cpp's loop never writes GaussPy) need not
- * be uploaded before every call.  gdp_host_track registers a host buffer (gdp_host_alloc memory,
- * or any page-aligned anonymous memory) and installs a SIGSEGV handler (once per process; faults
- * elsewhere go to the handler installed before it, or take the default action).  gdp_host_arm
- * write-protects the buffer's pages — the caller asserts that the buffer now equals the device
- * copy it mirrors; the first CPU write to each page then faults once, is recorded, and the page is
- * writable again.  gdp_upload_image_written / gdp_generate_dog_mirrored_written are
- * gdp_upload_image_raw / gdp_generate_dog_mirrored that upload only the pages written since the
- * buffer was armed (the caller asserts image b's device pyramid equals the buffer as of arming),
- * and re-arm it; on a buffer that is not tracked or not armed they upload everything (and arm it
- * if tracked).  gdp_host_written_bytes: bytes of the buffer in pages written since arming
- * (GDP_ERR_STATE when not armed).  gdp_host_untrack makes every page writable and forgets it.
- * Not seen (untrack such buffers): writes that do not fault on the CPU — DMA into the buffer, or
- * a system call such as read(2), which fails with EFAULT on a protected page.  GDP_ERR_STATE from
- * gdp_host_track: page protection is unavailable for this memory or no slot is free (64). */
+ * be uploaded before every call.  gdp_host_alloc_tracked: `bytes` of host memory for such a mirror
+ * — one shared-memory object mapped twice, a view registered with HIP that libgdp's copies use
+ * (gdp_upload_image_raw / gdp_download_image_raw / gdp_generate_dog_mirrored* given the returned
+ * address DMA through it at the pinned rate) and the returned CPU view, which is the one ever
+ * write-protected (protecting memory the GPU driver registered — hipHostMalloc / hipHostRegister —
+ * invalidates the registration and stalls the process's GPU queues, so gdp_host_track refuses such
+ * memory).  Freed by gdp_host_free.  GDP_ERR_STATE / _HIP / _NOMEM: not available (use
+ * gdp_host_alloc and whole uploads).  It is tracked from the start, not armed.
+ * gdp_host_track registers other, plain (unregistered, page-granular) host memory and re-enables
+ * tracking of an untracked gdp_host_alloc_tracked buffer; the first call installs a SIGSEGV
+ * handler (once per process; faults elsewhere go to the handler installed before it, or take the
+ * default action).  gdp_host_arm write-protects the buffer's pages — the caller asserts that the
+ * buffer now equals the device copy it mirrors; the first CPU write to each page then faults once,
+ * is recorded, and the page is writable again.  gdp_upload_image_written /
+ * gdp_generate_dog_mirrored_written are gdp_upload_image_raw / gdp_generate_dog_mirrored that
+ * upload only the pages written since the buffer was armed (the caller asserts image b's device
+ * pyramid equals the buffer as of arming), and re-arm it; on a buffer that is not tracked or not
+ * armed they upload everything (and arm it if tracked).  gdp_host_written_bytes: bytes of the
+ * buffer in pages written since arming (GDP_ERR_STATE when not armed).  gdp_host_untrack makes
+ * every page writable and stops recording (a gdp_host_alloc_tracked buffer keeps its DMA view).
+ * Not seen (untrack such buffers): writes that do not fault on the CPU view — DMA into it, or a
+ * system call such as read(2), which fails with EFAULT on a protected page.  GDP_ERR_STATE from
+ * gdp_host_track: page protection is unavailable for this memory, it is registered with the GPU,
+ * or no slot is free (64). */
+int gdp_host_alloc_tracked(size_t bytes, void** host);
 int gdp_host_track(void* host, size_t bytes);
 int gdp_host_untrack(void* host);
 int gdp_host_arm(void* host);
@@ -339,7 +350,8 @@ enum {
                                    2 XCD row-interleaved                                       */
     GDP_TUNE_INPLACE_SUB = 6,   /* in-place DoG / re-entry passes: blocks per 1024-group chunk,
                                    1 / 2 / 4 / 8 / 16 (default 16 for one image, else 4 up to
-                                   32 Mpix per launch, else 1); 0 = one level per wave (k_levels_x) */
+                                   32 Mpix per launch, else 1); 0 = one level per wave (k_levels_x);
+                                   -16 = 16 x 256 block tiles of k_build's shape (k_levels_tile) */
     GDP_TUNE_WINDOW_SUB = 7,    /* in-place window pass: blocks per chunk (4 default; 1, 2, 8, 16) */
     GDP_TUNE_CONV_KERNEL = 8,   /* gdp_build_gaussian: 0 register sweep (S <= 3), 1 LDS tiles,
                                    2 block tiles (default; one output row per wave, S <= 5) */

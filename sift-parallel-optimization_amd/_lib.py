@@ -99,6 +99,7 @@ SIGNATURES = {
     "gdp_image_floats": (_c_size, [_p]),
     "gdp_download_image_raw": (_c_int, [_p, _c_int, _p]),
     "gdp_generate_dog_mirrored": (_c_int, [_p, _c_int, _p]),
+    "gdp_host_alloc_tracked": (_c_int, [_c_size, _pp]),
     "gdp_host_track": (_c_int, [_p, _c_size]),
     "gdp_host_untrack": (_c_int, [_p]),
     "gdp_host_arm": (_c_int, [_p]),

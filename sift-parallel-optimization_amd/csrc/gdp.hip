@@ -301,6 +301,17 @@ int launch_inplace_sub(gdp_ctx* c, int ob, int oe, hipStream_t st, int sb = 0, i
 template <int MODE>
 int launch_inplace(gdp_ctx* c, int ob, int oe, hipStream_t st, int sb = 0, int se = -1) {
     const Geom& g = c->geom;
+    if ((MODE == 2 || MODE == 3) && c->inplace_sub == -kLtRows) {  // k_build-shaped block tiles
+        const long long grid = ((long long)g.lt_blk[oe] - g.lt_blk[ob]) * g.batch;
+        if (grid <= 0) return GDP_OK;
+        if (grid >= (1ll << 31)) return c->status(GDP_ERR_ARG, "in-place pass too large for one launch");
+        auto kern = c->nontemporal ? k_levels_tile<0, MODE, true> : k_levels_tile<0, MODE, false>;
+        if (g.L == 5) kern = c->nontemporal ? k_levels_tile<5, MODE, true> : k_levels_tile<5, MODE, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * kLtRows), 0, st, c->d_geom, c->d_in, c->d_out, c->d_taps,
+                           ob, oe);
+        GDP_HIP(c, hipGetLastError());
+        return GDP_OK;
+    }
     if ((MODE == 2 || MODE == 3) && c->inplace_sub == 0 && g.L <= 16) {
         const long long grid = ((long long)g.lx_blk[oe] - g.lx_blk[ob]) * g.batch;
         if (grid <= 0) return GDP_OK;
@@ -946,6 +957,7 @@ int gdp_create_band(gdp_ctx** out, int H, int W, int S, int O, int batch, int ro
         grp += (long long)og.rows * og.gpr;
         g.lv_blk[o + 1] = g.lv_blk[o] + (unsigned)(((long long)og.rows * og.gpr + kLevBlock - 1) / kLevBlock);
         g.lx_blk[o + 1] = g.lx_blk[o] + (unsigned)(((long long)og.rows * og.gpr + 63) / 64);
+        g.lt_blk[o + 1] = g.lt_blk[o] + (unsigned)(((long long)og.rows + kLtRows - 1) / kLtRows * ((og.gpr + 63) / 64));
         g.cv_tiles_c[o] = (og.cols + kCvTW - 1) / kCvTW;
         g.cv_blk[o + 1] = g.cv_blk[o] + (unsigned)(((long long)og.rows + kCvTH - 1) / kCvTH * g.cv_tiles_c[o]);
     }
@@ -1789,7 +1801,7 @@ int gdp_upload_image_raw(gdp_ctx* c, int b, const float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_raw: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
-    GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, host, (size_t)c->img_floats * 4,
+    GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, track_dma_ptr(host), (size_t)c->img_floats * 4,
                               hipMemcpyHostToDevice, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1845,7 +1857,17 @@ int gdp_host_alloc(size_t bytes, void** host) try {
 } GDP_ABI_CATCH(nullptr)
 
 void gdp_host_free(void* host) {
-    if (host) (void)hipHostFree(host);
+    if (!host) return;
+    {
+        std::lock_guard<std::mutex> lk(g_track_mu);
+        if (track_free_alias(host)) return;
+        if (TrackedMirror* t = track_find(host)) {  // a tracked plain buffer: forget it first
+            (void)mprotect(reinterpret_cast<void*>(t->base.load(std::memory_order_relaxed)),
+                           t->bytes.load(std::memory_order_relaxed), PROT_READ | PROT_WRITE);
+            track_retire(t);
+        }
+    }
+    (void)hipHostFree(host);
 }
 
 size_t gdp_image_floats(const gdp_ctx* c) { return c ? (size_t)c->img_floats : 0; }
@@ -1854,7 +1876,7 @@ int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_image_raw: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
-    GDP_HIP(c, hipMemcpyAsync(host, c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->img_floats * 4,
+    GDP_HIP(c, hipMemcpyAsync(track_dma_ptr(host), c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->img_floats * 4,
                               hipMemcpyDeviceToHost, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1949,14 +1971,12 @@ static int generate_dog_mirrored(gdp_ctx* c, int b, float* host, const std::vect
 int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored: bad argument") : GDP_ERR_ARG;
-    return generate_dog_mirrored(c, b, host, nullptr);
+    return generate_dog_mirrored(c, b, track_dma_ptr(host), nullptr);
 } GDP_ABI_CATCH(c)
 
 // ---- write-tracked host mirrors (gdp_track.inc) ----
-int gdp_host_track(void* host, size_t bytes) try {
-    if (!host || bytes == 0) return GDP_ERR_ARG;
-    std::lock_guard<std::mutex> lk(g_track_mu);
-    if (track_find(host)) return GDP_OK;
+// the SIGSEGV handler (once per process) and a free registry slot; caller holds g_track_mu
+static TrackedMirror* track_slot() {
     if (!g_segv_installed) {
         const long pg = sysconf(_SC_PAGESIZE);
         if (pg > 0) g_page_bytes = (size_t)pg;
@@ -1965,47 +1985,103 @@ int gdp_host_track(void* host, size_t bytes) try {
         sa.sa_sigaction = track_on_segv;
         sa.sa_flags = SA_SIGINFO | SA_RESTART | SA_ONSTACK;
         sigemptyset(&sa.sa_mask);
-        if (sigaction(SIGSEGV, &sa, &g_prev_segv) != 0) return GDP_ERR_STATE;
+        if (sigaction(SIGSEGV, &sa, &g_prev_segv) != 0) return nullptr;
         g_segv_installed = true;
     }
-    TrackedMirror* t = nullptr;
     for (TrackedMirror& s : g_tracked)
-        if (!s.base.load(std::memory_order_relaxed)) {
-            t = &s;
-            break;
-        }
-    if (!t) return GDP_ERR_STATE;
+        if (!s.base.load(std::memory_order_relaxed)) return &s;
+    return nullptr;
+}
+
+// publish a registry entry for the CPU range [host, host + bytes) (caller holds g_track_mu)
+static void track_publish(TrackedMirror* t, void* host, size_t bytes, void* dma, size_t map_bytes) {
     const uintptr_t u = reinterpret_cast<uintptr_t>(host);
     const uintptr_t base = u / g_page_bytes * g_page_bytes;
     const uintptr_t end = (u + bytes + g_page_bytes - 1) / g_page_bytes * g_page_bytes;
-    // protection must be available on this memory (a probe of its first page)
-    if (mprotect(reinterpret_cast<void*>(base), g_page_bytes, PROT_READ) != 0) return GDP_ERR_STATE;
-    if (mprotect(reinterpret_cast<void*>(base), g_page_bytes, PROT_READ | PROT_WRITE) != 0) return GDP_ERR_STATE;
     t->pages = (end - base) / g_page_bytes;
     t->written = new std::atomic<unsigned char>[t->pages];
     for (size_t p = 0; p < t->pages; ++p) t->written[p].store(0, std::memory_order_relaxed);
     t->user = host;
     t->user_bytes = bytes;
     t->armed = false;
+    t->tracking = true;
+    t->dma = dma;
+    t->map_bytes = map_bytes;
     t->bytes.store(end - base, std::memory_order_relaxed);
     t->base.store(base, std::memory_order_release);
+}
+
+int gdp_host_alloc_tracked(size_t bytes, void** host) try {
+    if (!host || bytes == 0) return GDP_ERR_ARG;
+    *host = nullptr;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    TrackedMirror* t = track_slot();
+    if (!t) return GDP_ERR_STATE;
+    const size_t map = (bytes + g_page_bytes - 1) / g_page_bytes * g_page_bytes;
+    // one shared-memory object, two mappings: `dma` registered with HIP (never protected),
+    // `cpu` the caller's view (the one write-protected)
+    const int fd = (int)memfd_create("gdp_mirror", MFD_CLOEXEC);
+    if (fd < 0) return GDP_ERR_STATE;
+    void* dma = MAP_FAILED;
+    void* cpu = MAP_FAILED;
+    if (ftruncate(fd, (off_t)map) == 0) {
+        dma = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
+        cpu = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
+    }
+    close(fd);
+    auto unmap = [&] {
+        if (dma != MAP_FAILED) munmap(dma, map);
+        if (cpu != MAP_FAILED) munmap(cpu, map);
+    };
+    if (dma == MAP_FAILED || cpu == MAP_FAILED) {
+        unmap();
+        return GDP_ERR_NOMEM;
+    }
+    const hipError_t e = hipHostRegister(dma, map, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        unmap();
+        return e == hipErrorOutOfMemory ? GDP_ERR_NOMEM : GDP_ERR_HIP;
+    }
+    track_publish(t, cpu, bytes, dma, map);
+    *host = cpu;
+    return GDP_OK;
+} GDP_ABI_CATCH(nullptr)
+
+int gdp_host_track(void* host, size_t bytes) try {
+    if (!host || bytes == 0) return GDP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    if (TrackedMirror* t = track_find(host)) {  // registered before (an alias whose tracking was off)
+        t->tracking = true;
+        return GDP_OK;
+    }
+    // memory the GPU driver registered must not be protected (gdp_track.inc): refuse it
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type != hipMemoryTypeUnregistered) {
+        (void)hipGetLastError();
+        return GDP_ERR_STATE;
+    }
+    (void)hipGetLastError();
+    TrackedMirror* t = track_slot();
+    if (!t) return GDP_ERR_STATE;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(host) / g_page_bytes * g_page_bytes;
+    // protection must be available on this memory (a probe of its first page)
+    if (mprotect(reinterpret_cast<void*>(base), g_page_bytes, PROT_READ) != 0) return GDP_ERR_STATE;
+    if (mprotect(reinterpret_cast<void*>(base), g_page_bytes, PROT_READ | PROT_WRITE) != 0) return GDP_ERR_STATE;
+    track_publish(t, host, bytes, nullptr, 0);
     return GDP_OK;
 } GDP_ABI_CATCH(nullptr)
 
 int gdp_host_untrack(void* host) try {
     std::lock_guard<std::mutex> lk(g_track_mu);
     TrackedMirror* t = host ? track_find(host) : nullptr;
-    if (!t) return GDP_ERR_ARG;
+    if (!t || !t->tracking) return GDP_ERR_ARG;
     const uintptr_t base = t->base.load(std::memory_order_relaxed);
     const int rc = mprotect(reinterpret_cast<void*>(base), t->bytes.load(std::memory_order_relaxed), PROT_READ | PROT_WRITE) == 0
                        ? GDP_OK
                        : GDP_ERR_STATE;
-    t->base.store(0, std::memory_order_release);
-    t->bytes.store(0, std::memory_order_relaxed);
-    delete[] t->written;
-    t->written = nullptr;
-    t->user = nullptr;
-    t->armed = false;
+    t->armed = t->tracking = false;
+    for (size_t p = 0; p < t->pages; ++p) t->written[p].store(0, std::memory_order_relaxed);
+    if (!t->dma) track_retire(t);  // an alias stays registered for its DMA view until gdp_host_free
     return rc;
 } GDP_ABI_CATCH(nullptr)
 
@@ -2013,6 +2089,10 @@ int gdp_host_arm(void* host) try {
     std::lock_guard<std::mutex> lk(g_track_mu);
     TrackedMirror* t = host ? track_find(host) : nullptr;
     if (!t) return GDP_ERR_ARG;
+    if (!t->tracking) return GDP_ERR_STATE;
+    // already armed: every page not written since is still protected, so only the written ones
+    // are protected again (no walk over the whole range)
+    if (t->armed) return track_rearm(*t, track_written_runs(*t), false);
     return track_rearm(*t, {}, true);
 } GDP_ABI_CATCH(nullptr)
 
@@ -2035,18 +2115,21 @@ int gdp_host_written_bytes(const void* host, size_t* bytes) try {
     return GDP_OK;
 } GDP_ABI_CATCH(nullptr)
 
-// The written pages of an armed mirror covering image b, or nullptr when the whole image must be
-// uploaded (not tracked / not armed / smaller than the image / too fragmented).  Caller holds
-// g_track_mu.
-static TrackedMirror* track_for_image(const gdp_ctx* c, const void* host, std::vector<std::pair<size_t, size_t>>* runs) {
+// The written pages of an armed mirror covering image b.  Returns the entry (nullptr: not
+// tracked); *partial: only `runs` need uploading (armed, large enough, not too fragmented).
+// Caller holds g_track_mu.
+static TrackedMirror* track_for_image(const gdp_ctx* c, const void* host, std::vector<std::pair<size_t, size_t>>* runs,
+                                      bool* partial) {
+    *partial = false;
     TrackedMirror* t = track_find(host);
-    if (!t) return nullptr;
+    if (!t || !t->tracking) return nullptr;
     const size_t img_bytes = (size_t)c->img_floats * 4;
     if (!t->armed || t->user_bytes < img_bytes) return t;
     *runs = track_written_runs(*t);
     for (auto& r : *runs) r.second = std::min(r.second, img_bytes);
     runs->erase(std::remove_if(runs->begin(), runs->end(), [](const std::pair<size_t, size_t>& r) { return r.second <= r.first; }),
                 runs->end());
+    *partial = runs->size() <= 4096;
     return t;
 }
 
@@ -2055,17 +2138,16 @@ int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
         return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_written: bad argument") : GDP_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_track_mu);
     std::vector<std::pair<size_t, size_t>> runs;
-    TrackedMirror* t = track_for_image(c, host, &runs);
-    const bool partial = t && t->armed && t->user_bytes >= (size_t)c->img_floats * 4 && runs.size() <= 4096;
+    bool partial = false;
+    TrackedMirror* t = track_for_image(c, host, &runs, &partial);
+    const char* src = static_cast<const char*>(track_dma_ptr(static_cast<const void*>(host)));
     GDP_HIP(c, hipSetDevice(c->device));
+    char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
     if (partial) {
-        char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
         for (const auto& r : runs)
-            GDP_HIP(c, hipMemcpyAsync(dev + r.first, reinterpret_cast<const char*>(host) + r.first, r.second - r.first,
-                                      hipMemcpyHostToDevice, c->stream));
+            GDP_HIP(c, hipMemcpyAsync(dev + r.first, src + r.first, r.second - r.first, hipMemcpyHostToDevice, c->stream));
     } else {
-        GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, host, (size_t)c->img_floats * 4,
-                                  hipMemcpyHostToDevice, c->stream));
+        GDP_HIP(c, hipMemcpyAsync(dev, src, (size_t)c->img_floats * 4, hipMemcpyHostToDevice, c->stream));
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     if (t && track_rearm(*t, runs, !partial) != GDP_OK)
@@ -2078,9 +2160,9 @@ int gdp_generate_dog_mirrored_written(gdp_ctx* c, int b, float* host) try {
         return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored_written: bad argument") : GDP_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_track_mu);
     std::vector<std::pair<size_t, size_t>> runs;
-    TrackedMirror* t = track_for_image(c, host, &runs);
-    const bool partial = t && t->armed && t->user_bytes >= (size_t)c->img_floats * 4 && runs.size() <= 4096;
-    const int rc = generate_dog_mirrored(c, b, host, partial ? &runs : nullptr);
+    bool partial = false;
+    TrackedMirror* t = track_for_image(c, host, &runs, &partial);
+    const int rc = generate_dog_mirrored(c, b, track_dma_ptr(host), partial ? &runs : nullptr);
     if (rc != GDP_OK) {
         if (t) t->armed = false;  // the device may hold a partial result: the next call uploads all
         return rc;
@@ -2261,9 +2343,9 @@ int gdp_set_tuning(gdp_ctx* c, int key, int value) try {
         case GDP_TUNE_INPLACE_SUB:
         case GDP_TUNE_WINDOW_SUB:
             if ((value != 1 && value != 2 && value != 4 && value != 8 && value != 16) &&
-                !(key == GDP_TUNE_INPLACE_SUB && value == 0))
+                !(key == GDP_TUNE_INPLACE_SUB && (value == 0 || value == -kLtRows)))
                 return c->status(GDP_ERR_ARG, "sub-blocks must be 1, 2, 4, 8 or 16 (1024 / sub threads per block; "
-                                              "in-place DoG also 0: one level per wave)");
+                                              "in-place DoG also 0: one level per wave, -16: 16 x 256 block tiles)");
             (key == GDP_TUNE_INPLACE_SUB ? c->inplace_sub : c->window_sub) = value;
             return GDP_OK;
         case GDP_TUNE_CONV_KERNEL:

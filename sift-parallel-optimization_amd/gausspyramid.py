@@ -18,7 +18,11 @@ and it may be written any way (g.GaussPy[o][s][r][c] = v, row slices, views, ufu
 Every mutating call first uploads each touched level whose bits differ from what the device last
 gave it (an exact comparison against a snapshot; levels only read are not uploaded, so reading
 GaussPy — output() included — never costs the fused GaussPyInit+GenerateDoG path), then runs,
-then refreshes every touched level in place.  GaussPyInit re-reads the CURRENT `data` (:80) and
+then refreshes every touched level in place — the touched levels are views into ONE host buffer in
+the device's raw layout, so when they hold at least half of the pyramid's bytes (e.g. a caller
+that walks every level) the refresh is one gdp_download_image_raw instead of one blocking copy per
+level; levels touched once stay in the refresh for the object's lifetime (like
+reference rows, a dropped handle may still have been written).  GaussPyInit re-reads the CURRENT `data` (:80) and
 overwrites host edits, as the reference's refill does.  Levels never touched cost nothing.
 SyncDevice() uploads the edited levels on demand.
 
@@ -445,6 +449,7 @@ class GaussPyramid:
         self._ctx = PyramidContext(length, length, self.S, self.layer, batch=1, device=device)
         self._cache = {}  # (o, s) -> the level's host array (live for the object's lifetime)
         self._snap = {}  # (o, s) -> the bits the device last gave that array (edit detection)
+        self._raw = None  # one host buffer in the device's raw image layout; the levels are views
         self._fresh = False
         self.uploaded_levels = 0  # levels the last SyncDevice uploaded (0: the host held no edits)
         self.GaussPyInit()  # :57
@@ -509,22 +514,34 @@ class GaussPyramid:
     def _level(self, o, s):
         key = (o, s)
         if key not in self._cache:
+            if self._raw is None:
+                self._raw = np.empty(lib().gdp_image_floats(self._ctx._ctx), np.float32)
+            rows, cols = self._ctx.level_dims(o)[:2]
+            off = self._ctx.level_offset(0, o, s)
+            arr = self._raw[off:off + rows * cols].reshape(rows, cols)
             self._ctx.sync()
-            arr = self._ctx.level(0, o, s)
+            if arr.size:
+                check(lib().gdp_download_level(self._ctx._ctx, 0, int(o), int(s), _ptr(arr)), self._ctx._ctx)
             self._cache[key] = arr
             self._snap[key] = arr.copy()
         return self._cache[key]
 
     def _refresh(self):
         """After a device-side change: every touched level re-downloaded INTO its existing array,
-        so handles the caller holds stay live (the reference's rows never move)."""
+        so handles the caller holds stay live (the reference's rows never move) — in one raw copy
+        of the image when the touched levels are at least half of its bytes, else level by level."""
         if not self._cache:
             return
         self._ctx.sync()
-        for (o, s), arr in self._cache.items():
-            if arr.size:
-                check(lib().gdp_download_level(self._ctx._ctx, 0, int(o), int(s), _ptr(arr)), self._ctx._ctx)
-            self._snap[(o, s)][...] = arr
+        touched = sum(arr.size for arr in self._cache.values())
+        if 2 * touched >= self._raw.size:
+            check(lib().gdp_download_image_raw(self._ctx._ctx, 0, _ptr(self._raw)), self._ctx._ctx)
+        else:
+            for (o, s), arr in self._cache.items():
+                if arr.size:
+                    check(lib().gdp_download_level(self._ctx._ctx, 0, int(o), int(s), _ptr(arr)), self._ctx._ctx)
+        for key, arr in self._cache.items():
+            self._snap[key][...] = arr
 
     def pyramid(self):
         """Packed [o][s][r][c] float32 copy (the oracle's layout)."""

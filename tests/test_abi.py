@@ -267,3 +267,37 @@ def test_window_centre_modes_are_exported(pkg):
     assert L.gdp_get_window_centre(None) == -1
     assert L.gdp_copy_band(None, 0, None, 0, None) == 1
     assert L.gdp_status_string(6) == b"internal error"
+
+
+_ROLES_CPP = r"""
+#include "GaussDePyramid-HIP-mpi.h"
+int main() {
+    typedef GaussPyramid_hip_mpi G;
+    for (int S = 0; S <= 5; ++S)
+        for (int w = 1; w <= 12; ++w) {
+            if (G::reference_roles(G::ROLES_AUTO, w, S) != (w >= S + 4)) return 1;
+            if (G::reference_roles(G::ROLES_BANDS, w, S)) return 2;
+            if (!G::reference_roles(G::ROLES_REFERENCE, w, S)) return 3;
+        }
+    return 0;
+}
+"""
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/conda/include/mpi.h"), reason="no MPI headers")
+def test_mpi_dropin_role_map_selection(tmp_path):
+    """the band map is the default; ROLES_AUTO still selects the reference's role map
+    (GaussDePyramid-MPI.h:265-335: workers 0..S+2, collector S+3) from S+4 ranks on, and
+    ROLES_REFERENCE always — the decision GenerateDoG_mpi makes (GaussPyramid_hip_mpi::
+    reference_roles), checked for S = 0..5 and 1..12 ranks.  Callers read the pyramid on
+    g.collector() (examples/mpi_hip.cpp)."""
+    src = tmp_path / "roles.cpp"
+    src.write_text(_ROLES_CPP)
+    exe = tmp_path / "roles"
+    # only the static decision is odr-used: no library is linked
+    subprocess.run(["g++", "-std=c++14", "-Wall", "-Wextra", "-Werror", "-I" + os.path.join(REPO, "include"),
+                    "-I/opt/conda/include", str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, (r.returncode, r.stderr[-500:])
+    with open(os.path.join(REPO, "include", "GaussDePyramid-HIP-mpi.h")) as f:
+        assert "int roles = ROLES_BANDS;" in f.read()  # the default map

@@ -21,32 +21,54 @@ def _expand(ref):
 
 def _cited(text):
     refs = set()
-    for m in re.finditer(r"profiles/([A-Za-z0-9_.{},*\-]+)", text):
-        refs.add(m.group(1).rstrip(".,)"))
+    for m in re.finditer(r"profiles/([A-Za-z0-9_.{},*<>\-]+)", text):
+        refs.add(re.sub(r"<[^>]*>", "*", m.group(1).rstrip(".,)")))  # <V> placeholders: any text
     for m in re.finditer(r"`([A-Za-z0-9_{},*\-]+(?:\.[a-z0-9]+)*\.(?:log|json|csv))`", text):
         refs.add(m.group(1))
     return refs
 
 
-def test_every_cited_profile_exists():
+def _missing(doc, names):
+    text = open(os.path.join(REPO, doc)).read()
+    out = []
+    for ref in _cited(text):
+        if ref.startswith(("pmc_records.json#", "archive_")) or "/" in ref.rstrip("/"):
+            continue
+        if ref.endswith(".json") and not ref.startswith(("pmc_", "sq_", "calib_")):
+            continue  # repo-level JSON (BENCH_r05.json, meta.json, ...) is not a profile
+        for alt in _expand(ref):
+            if not any(fnmatch.fnmatch(n, alt) for n in names):
+                out.append((doc, alt))
+    return out
+
+
+def _profile_names():
+    import json  # PMC records gathered into profiles/pmc_records.json keep their file names
+
     tracked = subprocess.run(["git", "ls-files", "profiles"], cwd=REPO, capture_output=True, text=True,
                              check=True).stdout.split()
     names = {os.path.relpath(p, "profiles") for p in tracked} | set(os.listdir(os.path.join(REPO, "profiles")))
-    import json  # PMC records gathered into profiles/pmc_records.json keep their file names
-
     with open(os.path.join(REPO, "profiles", "pmc_records.json")) as f:
         names |= {r["file"] for r in json.load(f)}
+    return names
+
+
+def test_every_cited_profile_exists():
+    names = _profile_names()
     missing = []
     for doc in ("DESIGN.md", "README.md", "INTEGRATION.md"):
-        text = open(os.path.join(REPO, doc)).read()
-        for ref in _cited(text):
-            if ref.startswith(("pmc_records.json#", "archive_")) or "/" in ref.rstrip("/"):
-                continue
-            if ref.endswith(".json") and not ref.startswith(("pmc_", "sq_", "calib_")):
-                continue  # repo-level JSON (BENCH_r04.json, meta.json, ...) is not a profile
-            for alt in _expand(ref):
-                if not any(fnmatch.fnmatch(n, alt) for n in names):
-                    missing.append((doc, alt))
+        missing += _missing(doc, names)
+    assert not missing, missing
+
+
+def test_design_history_citations_resolve_to_profiles_or_the_archive():
+    """DESIGN_HISTORY.md cites round 1-4 logs that the round-5 prune moved into
+    profiles/archive_r01-r04.tar.xz; every citation is a current profile or an archive member."""
+    import tarfile
+
+    with tarfile.open(os.path.join(REPO, "profiles", "archive_r01-r04.tar.xz")) as t:
+        archived = {os.path.basename(m.name) for m in t.getmembers()}
+    missing = _missing("DESIGN_HISTORY.md", _profile_names() | archived)
     assert not missing, missing
 
 

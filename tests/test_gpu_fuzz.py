@@ -23,7 +23,7 @@ SCALE = max(1, int(os.environ.get("GDP_FUZZ_SCALE", "1")))
 SEED = int(os.environ.get("GDP_FUZZ_SEED", "0"))
 MAXDIM = max(300, int(os.environ.get("GDP_FUZZ_MAXDIM", "300")))  # shapes 1..MAXDIM (build / subset)
 N_CASES = 300 * SCALE
-INPLACE_SUBS = (0, 1, 2, 4, 8, 16)
+INPLACE_SUBS = (0, 1, 2, 4, 8, 16, -16)
 
 
 def _progress(name, i):
@@ -64,7 +64,7 @@ def _follow_up(rng):
     random block split) or the GaussFilter pass of a random octave range."""
     r = rng.random()
     kind = "none" if r < 0.6 else "regen" if r < 0.85 else "gauss"
-    return kind, int(rng.choice(INPLACE_SUBS)), int(rng.choice(INPLACE_SUBS[1:]))
+    return kind, int(rng.choice(INPLACE_SUBS)), int(rng.choice(INPLACE_SUBS[1:-1]))  # window: no tiles
 
 
 def test_randomized_parity_sweep(pkg, oracle):

@@ -322,7 +322,7 @@ def test_zero_window_path_is_bit_exact(pkg, oracle, zw):
                 win = re.copy()
                 for o in range(Oo):  # (the oracle's GaussFilter has the serial centre only)
                     oracle.gauss_octave(win, H, W, S, o)
-                for sub, wsub in ((1, 4), (0, 1), (4, 16)):
+                for sub, wsub in ((1, 4), (0, 1), (4, 16), (-16, 2)):
                     ctx.set_tuning(inplace_sub=sub, window_sub=wsub)
                     ctx.build()
                     ctx.generate_dog()
@@ -493,7 +493,7 @@ def test_int_star_star_upload(pkg, oracle):
 
 
 # ------------------------------------------------------------------ in-place ops / re-entry
-@pytest.mark.parametrize("sub", [0, 1, 16])
+@pytest.mark.parametrize("sub", [0, 1, 16, -16])
 def test_inplace_ops_match_reference_order(pkg, oracle, sub):
     H, W, S = 72, 104, 2
     O = oracle.default_octaves(H, W)
@@ -516,7 +516,7 @@ def test_inplace_ops_match_reference_order(pkg, oracle, sub):
         _assert_same(ctx.pyramid(0), want, "GenerateDoG re-entry")
 
 
-@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0), (1, 8), (1, 16)])
+@pytest.mark.parametrize("nt,sub", [(1, 1), (0, 1), (1, 2), (1, 4), (1, 0), (0, 0), (1, 8), (1, 16), (1, -16), (0, -16)])
 def test_gauss_range_and_store_modes(pkg, oracle, nt, sub):
     """One-launch GaussFilter over an octave range == per-octave GaussFilter; both store modes;
     every in-place DoG kernel (sub 0 = one level per wave, k_levels_x; S = 14 has 17 levels and

@@ -388,7 +388,7 @@ def test_inplace_zero_window_is_exact_for_caller_values_near_flt_max(pkg, oracle
     with pkg.PyramidContext(n, n, S=S) as ctx:
         for zw in (0, 1):
             ctx.set_tuning(zero_window=zw)
-            for sub, wsub in ((1, 4), (0, 1), (16, 16)):
+            for sub, wsub in ((1, 4), (0, 1), (16, 16), (-16, 8)):
                 ctx.set_tuning(inplace_sub=sub, window_sub=wsub)
                 ctx.upload_pyramid(base)
                 ctx.gauss_octave(0)
@@ -436,3 +436,71 @@ def test_reference_role_map_steps_on_the_gpu(pkg, oracle):
             for s, h in enumerate(row):
                 assert oracle.fnv(lvs[(o, s)]) == int(h, 16), ("collector", n, S, spec, o, s)
         torch.cuda.synchronize()
+
+
+def test_tracked_mirror_uploads_only_written_pages(pkg, oracle):
+    """gdp_host_alloc_tracked: a shared-memory object mapped twice — a view
+    registered with HIP for the DMA copies and the CPU view returned, the only one ever
+    write-protected (protecting hipHostMalloc memory stalls the process's GPU queues, so
+    gdp_host_track refuses it).  Downloads through the CPU view land in it; after arming, a
+    single-float write is recorded as its page and gdp_generate_dog_mirrored_written == the
+    whole-mirror gdp_generate_dog_mirrored on the same edited pyramid, bit for bit; with nothing
+    written the next call uploads nothing and still equals the in-place pass on the device copy."""
+    import ctypes
+
+    L = pkg.lib()
+    page = os.sysconf("SC_PAGESIZE")
+    H = W = 512
+    S = 2
+    with pkg.PyramidContext(H, W, S=S) as a, pkg.PyramidContext(H, W, S=S) as m:
+        n = L.gdp_image_floats(a._ctx)
+        img = oracle.lcg_image(H, W, 77)
+        for c in (a, m):
+            c.set_input(img, 0)
+            c.build()
+            c.sync()
+        pinned = ctypes.c_void_p()
+        assert L.gdp_host_alloc(n * 4, ctypes.byref(pinned)) == 0
+        try:
+            assert L.gdp_host_track(pinned, n * 4) == 3  # registered with the GPU: refused
+        finally:
+            L.gdp_host_free(pinned)
+        hptr = ctypes.c_void_p()
+        assert L.gdp_host_alloc_tracked(n * 4, ctypes.byref(hptr)) == 0
+        try:
+            host = np.ctypeslib.as_array(ctypes.cast(hptr, ctypes.POINTER(ctypes.c_float)), shape=(n,))
+            assert L.gdp_download_image_raw(m._ctx, 0, hptr) == 0  # DMA through the registered view
+            ref = np.empty(n, np.float32)
+            assert L.gdp_download_image_raw(a._ctx, 0, ref.ctypes.data_as(ctypes.c_void_p)) == 0
+            _assert_same(host, ref, "download through the tracked mirror")
+            written = ctypes.c_size_t()
+            assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 3  # not armed yet
+            assert L.gdp_host_arm(hptr) == 0
+            assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 0 and written.value == 0
+            off = m.level_offset(0, 0, 2) + 7 * W + 9
+            host[off] = np.float32(-1e30)  # one float through the CPU view: faults once, recorded
+            ref[off] = np.float32(-1e30)
+            assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 0 and written.value == page
+            # whole-mirror reference on context a: upload the edited copy, in-place pass, download
+            assert L.gdp_generate_dog_mirrored(a._ctx, 0, ref.ctypes.data_as(ctypes.c_void_p)) == 0
+            assert L.gdp_generate_dog_mirrored_written(m._ctx, 0, hptr) == 0
+            _assert_same(host, ref, "written-page upload == whole upload after a one-float edit")
+            assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 0 and written.value == 0  # re-armed
+            assert L.gdp_generate_dog_mirrored(a._ctx, 0, ref.ctypes.data_as(ctypes.c_void_p)) == 0
+            assert L.gdp_generate_dog_mirrored_written(m._ctx, 0, hptr) == 0  # nothing written: no upload
+            _assert_same(host, ref, "no-write call")
+            got = np.empty(n, np.float32)
+            assert L.gdp_download_image_raw(m._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            _assert_same(got, ref, "device copy")
+            host[: W] = np.float32(2.5)  # a row through the CPU view, then gdp_upload_image_written
+            ref[: W] = np.float32(2.5)
+            assert L.gdp_upload_image_written(m._ctx, 0, hptr) == 0
+            assert L.gdp_download_image_raw(m._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            _assert_same(got, ref, "gdp_upload_image_written")
+            assert L.gdp_host_untrack(hptr) == 0  # writable, not recorded; the DMA view stays
+            host[5] = np.float32(1.0)
+            assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 3
+            assert L.gdp_download_image_raw(m._ctx, 0, hptr) == 0
+            _assert_same(host, ref, "download after untrack")
+        finally:
+            L.gdp_host_free(hptr)

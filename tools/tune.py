@@ -93,6 +93,8 @@ def main():
     for name, kw in variants:  # warm-up + identical-output check for every variant (per op)
         apply(kw)
         {"conv": ctx.build_gaussian, "subset": ctx.build_subset}.get(kw["op"], ctx.build)()
+        if kw["op"] == "regen":  # the checksum below is then the re-entry's (GenerateDoG on the build)
+            ctx.generate_dog()
         ctx.sync()
         if args.checksums:
             print(json.dumps({"variant": name, "shape": [H, W, B], "checksum0": f"{ctx.checksum(0):016x}"}), flush=True)
