@@ -76,3 +76,46 @@ def test_profiles_directory_stays_small():
     tracked = subprocess.run(["git", "ls-files", "profiles"], cwd=REPO, capture_output=True, text=True,
                              check=True).stdout.split()
     assert len(tracked) < 400, len(tracked)
+
+
+def _bench_records():
+    import glob
+    import json
+
+    out = {}
+    for p in glob.glob(os.path.join(REPO, "BENCH_r*.json")):
+        m = re.search(r"BENCH_r(\d+)\.json$", p)
+        if m:
+            with open(p) as f:
+                out[int(m.group(1))] = (os.path.basename(p), json.load(f))
+    return out
+
+
+def _last_commit_time(path):
+    r = subprocess.run(["git", "log", "-1", "--format=%ct", "--", path], cwd=REPO, capture_output=True, text=True)
+    return int(r.stdout.strip() or 0)
+
+
+def test_quoted_driver_headline_is_the_newest_record():
+    """DESIGN.md and README.md quote the driver's headline from the newest
+    BENCH_r*.json — its name, % of the roofline, kernel_ms, Mpix/s and CPU baseline as the driver
+    recorded them.  (A record the driver commits after the docs' last change may be one round
+    newer than the one they cite.)"""
+    recs = _bench_records()
+    if not recs:
+        return
+    newest = max(recs)
+    for doc in ("DESIGN.md", "README.md"):
+        text = open(os.path.join(REPO, doc)).read()
+        m = re.search(r"driver[^\n]*?\(`(BENCH_r(\d+)\.json)`", text)
+        assert m, (doc, "names no driver record")
+        cited = int(m.group(2))
+        if cited != newest:
+            assert cited == newest - 1 and _last_commit_time(recs[newest][0]) >= _last_commit_time(doc), \
+                (doc, "cites", m.group(1), "newest", recs[newest][0])
+        name, rec = recs[cited]
+        p = rec["parsed"]
+        want = [f"{100 * p['roofline']['frac']:.1f} %", f"{p['roofline']['kernel_ms']:.4f}",
+                f"{round(p['value']):,}", f"{p['cpu_baseline']['value']:,.1f}"]
+        for w in want:
+            assert w in text, (doc, name, w)
