@@ -1999,7 +1999,12 @@ static void track_publish(TrackedMirror* t, void* host, size_t bytes, void* dma,
     const uintptr_t base = u / g_page_bytes * g_page_bytes;
     const uintptr_t end = (u + bytes + g_page_bytes - 1) / g_page_bytes * g_page_bytes;
     t->pages = (end - base) / g_page_bytes;
-    t->written = new std::atomic<unsigned char>[t->pages];
+    // a larger flag array when needed; the old one stays allocated (a handler on another thread may
+    // still read it), so a slot holds at most one array per size it has grown to
+    if (t->written_cap < t->pages) {
+        t->written = new std::atomic<unsigned char>[t->pages];
+        t->written_cap = t->pages;
+    }
     for (size_t p = 0; p < t->pages; ++p) t->written[p].store(0, std::memory_order_relaxed);
     t->user = host;
     t->user_bytes = bytes;
@@ -2133,13 +2138,20 @@ static TrackedMirror* track_for_image(const gdp_ctx* c, const void* host, std::v
     return t;
 }
 
+// (The registry lock is held while the written runs are collected and while the mirror is
+// re-armed, not across the copies and kernels between, so drop-in objects on other threads keep
+// their GPU work concurrent.  A buffer must not be freed or untracked by another thread during a
+// call on it — the caller's contract for any buffer it passes in.)
 int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_written: bad argument") : GDP_ERR_ARG;
-    std::lock_guard<std::mutex> lk(g_track_mu);
     std::vector<std::pair<size_t, size_t>> runs;
     bool partial = false;
-    TrackedMirror* t = track_for_image(c, host, &runs, &partial);
+    TrackedMirror* t;
+    {
+        std::lock_guard<std::mutex> lk(g_track_mu);
+        t = track_for_image(c, host, &runs, &partial);
+    }
     const char* src = static_cast<const char*>(track_dma_ptr(static_cast<const void*>(host)));
     GDP_HIP(c, hipSetDevice(c->device));
     char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
@@ -2150,6 +2162,7 @@ int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
         GDP_HIP(c, hipMemcpyAsync(dev, src, (size_t)c->img_floats * 4, hipMemcpyHostToDevice, c->stream));
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
+    std::lock_guard<std::mutex> lk(g_track_mu);
     if (t && track_rearm(*t, runs, !partial) != GDP_OK)
         return c->status(GDP_ERR_STATE, "gdp_upload_image_written: mprotect refused re-arming the mirror");
     return GDP_OK;
@@ -2158,11 +2171,15 @@ int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
 int gdp_generate_dog_mirrored_written(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored_written: bad argument") : GDP_ERR_ARG;
-    std::lock_guard<std::mutex> lk(g_track_mu);
     std::vector<std::pair<size_t, size_t>> runs;
     bool partial = false;
-    TrackedMirror* t = track_for_image(c, host, &runs, &partial);
+    TrackedMirror* t;
+    {
+        std::lock_guard<std::mutex> lk(g_track_mu);
+        t = track_for_image(c, host, &runs, &partial);
+    }
     const int rc = generate_dog_mirrored(c, b, track_dma_ptr(host), partial ? &runs : nullptr);
+    std::lock_guard<std::mutex> lk(g_track_mu);
     if (rc != GDP_OK) {
         if (t) t->armed = false;  // the device may hold a partial result: the next call uploads all
         return rc;

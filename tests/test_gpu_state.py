@@ -504,3 +504,40 @@ def test_tracked_mirror_uploads_only_written_pages(pkg, oracle):
             _assert_same(host, ref, "download after untrack")
         finally:
             L.gdp_host_free(hptr)
+
+
+def test_cpp_class_random_edit_sequences_with_write_tracking(oracle, tmp_path):
+    """Seeded random op sequences on GaussPyramid_hip (examples/state_hip): host edits (single
+    floats, scaled rows, negated / zeroed levels, the input copy), calls (GenerateDoG, GaussFilter,
+    GenerateDoG_mpi, GaussPyInit), mirror on / off with host_dirty / SyncDevice / SyncHost, and the
+    write tracking switched off and on in between — the result must not depend on what the tracking
+    uploads: bit-identical to the oracle's replay of the same ops in every sequence."""
+    rng = np.random.default_rng(606)
+    for case in range(16):
+        n = int(rng.choice([64, 100, 32]))
+        O = oracle.octaves(n)
+        ops = []
+        for _ in range(int(rng.integers(6, 16))):
+            k = rng.random()
+            o = int(rng.integers(0, min(O, 4)))
+            s_ = int(rng.integers(0, 5))
+            ln = n >> o
+            if k < 0.22:
+                ops.append(str(rng.choice(["dog", "dog", "mpi", f"filter:{o}"])))
+            elif k < 0.45:
+                ops.append(f"set:{o}:{s_}:{int(rng.integers(0, ln))}:{int(rng.integers(0, ln))}:"
+                           f"{float(rng.uniform(-1e3, 1e3)):.6g}")
+            elif k < 0.55:
+                ops.append(f"scale:{o}:{s_}:{int(rng.integers(0, ln))}:{float(rng.choice([-2.0, 0.5, 3.0]))}")
+            elif k < 0.62:
+                ops.append(str(rng.choice([f"neg:{o}:{s_}", f"zero:{o}:{s_}"])))
+            elif k < 0.70:
+                ops.append(str(rng.choice(["track:0", "track:1", "written"])))
+            elif k < 0.80:
+                ops.append(str(rng.choice(["mirror:0", "mirror:1", "dirty", "syncdev", "synchost"])))
+            elif k < 0.87:
+                ops.append(f"data:{int(rng.integers(0, n))}:{int(rng.integers(0, n))}:{int(rng.integers(-500, 500))}")
+            else:
+                ops.append(str(rng.choice(["init", "dog"])))
+        ops += ["mirror:1", "dog"]  # end on a mirrored call so GaussPy holds the final state
+        _run(oracle, tmp_path, "hip", n, 2, f"lcg:{700 + case}", ops)

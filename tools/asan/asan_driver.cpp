@@ -125,7 +125,33 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
         OK(gdp_host_alloc(raw.size() * 4, &pinned));
         std::memcpy(pinned, raw.data(), raw.size() * 4);
         OK(gdp_generate_dog_mirrored(c, 0, static_cast<float*>(pinned)));
+        EXPECT(gdp_host_track(pinned, raw.size() * 4) == GDP_ERR_STATE);  // registered memory refused
         gdp_host_free(pinned);
+        // round 6: the write-tracked mirror (aliased registered + protected views, SIGSEGV handler)
+        void* tv = nullptr;
+        if (gdp_host_alloc_tracked(raw.size() * 4, &tv) == GDP_OK) {
+            float* t = static_cast<float*>(tv);
+            size_t wb = 7;
+            OK(gdp_download_image_raw(c, 0, t));
+            EXPECT(gdp_host_written_bytes(t, &wb) == GDP_ERR_STATE);
+            OK(gdp_host_arm(t));
+            OK(gdp_host_written_bytes(t, &wb));
+            EXPECT(wb == 0);
+            t[3] = -2.5f;  // a write through the protected view: recorded, and it lands
+            OK(gdp_host_written_bytes(t, &wb));
+            EXPECT(wb > 0 && t[3] == -2.5f);
+            OK(gdp_generate_dog_mirrored_written(c, 0, t));
+            OK(gdp_host_written_bytes(t, &wb));
+            EXPECT(wb == 0);
+            t[raw.size() - 1] = 1.0f;
+            OK(gdp_upload_image_written(c, 0, t));
+            OK(gdp_host_untrack(t));
+            t[0] = 2.0f;  // writable, not recorded
+            OK(gdp_host_track(t, raw.size() * 4));  // tracking back on (not armed)
+            OK(gdp_upload_image_written(c, 0, t));  // not armed: the whole mirror, then armed
+            OK(gdp_host_written_bytes(t, &wb));
+            gdp_host_free(tv);
+        }
         EXPECT(gdp_generate_dog_mirrored(c, 1 << 20, raw.data()) == GDP_ERR_ARG);
         EXPECT(gdp_generate_dog_mirrored(c, 0, nullptr) == GDP_ERR_ARG);
         int ids[64];
