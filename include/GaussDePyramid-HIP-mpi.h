@@ -40,8 +40,11 @@
 // (gdp_copy_band).  GaussPy is two-way state, as in the reference (GaussDePyramid-MPI.h:18, the
 // float**** every method works on): with `mirror_host` (default) a rank whose GaussPy mirrors its
 // device state (every rank after GaussPyInit and the single-process calls, the collector after
-// GenerateDoG_mpi) uploads it before each mutating call, so edits are processed; a worker's GaussPy
-// is not refreshed by a band GenerateDoG_mpi, so it uploads only when the caller sets `host_dirty`.
+// GenerateDoG_mpi) uploads what the caller wrote into it before each mutating call, so edits are
+// processed — write-tracked like GaussPyramid_hip's mirror: only the pages
+// written since it last equalled the device state, none when nothing was written (which also keeps
+// the fused build and the live band rows); a worker's GaussPy is not refreshed by a band
+// GenerateDoG_mpi, so it uploads only when the caller sets `host_dirty`.
 // In the reference the collector's output depends only on the workers' states (scale i from rank
 // i); with the band map on every rank's own rows — the same whenever the ranks hold the same
 // GaussPy (SPMD callers).
@@ -126,8 +129,26 @@ protected:
             }
         return true;
     }
-    void pull_host_() {
-        if ((mirror_host && host_current_) || host_dirty) SyncDevice();
+    void pull_host_() {  // before a mutating call (the written pages only, when the mirror is armed)
+        const bool clean = armed_;
+        armed_ = false;  // the call changes the device; SyncHost re-arms
+        if (!((mirror_host && host_current_) || host_dirty)) return;
+        if (clean && rows_in_mirror_()) {
+            size_t w = 0;
+            const bool any = gdp_host_written_bytes(host_, &w) != GDP_OK || w > 0;
+            check_(gdp_upload_image_written(full_, 0, host_), "SyncDevice", full_);
+            host_dirty = false;
+            host_current_ = true;
+            if (any) fresh_ = band_live_ = false;  // nothing written: the device state is unchanged
+            return;
+        }
+        SyncDevice();
+        armed_ = false;
+    }
+    bool track_ = false;  // host_ is write-tracked (gdp_host_alloc_tracked, GaussDePyramid-HIP.h)
+    bool armed_ = false;  // ... and equals full_'s pyramid as of its arming
+    void arm_() {
+        armed_ = track_ && rows_in_mirror_() && gdp_host_arm(host_) == GDP_OK;
     }
     // the error text is read only after the failing call returned (never as a sibling argument,
     // whose evaluation order relative to the call is unspecified)
@@ -149,6 +170,7 @@ protected:
     void sync_host_() {
         check_(rows_in_mirror_() ? gdp_download_image_raw(full_, 0, host_) : gdp_download_pyramid_rows(full_, 0, GaussPy),
                "download", full_);
+        arm_();
     }
     void ensure_full_();
 };
@@ -171,8 +193,16 @@ inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi(int** img, int len, int S_) : 
     ensure_full_();
     // the rows (one new float[] each in the reference) point into one pinned buffer laid out like
     // the device pyramid: the collector's mirror is a single DMA copy (new[] rows if refused)
+    // (write-tracked like GaussPyramid_hip's mirror where available: a call uploads only the pages
+    // the caller wrote since the last one)
     void* h = nullptr;
-    if (gdp_host_alloc(gdp_image_floats(full_) * sizeof(float), &h) == GDP_OK) host_ = static_cast<float*>(h);
+    const size_t mirror_bytes = gdp_image_floats(full_) * sizeof(float);
+    if (gdp_host_alloc_tracked(mirror_bytes, &h) == GDP_OK) {
+        host_ = static_cast<float*>(h);
+        track_ = true;
+    } else if (gdp_host_alloc(mirror_bytes, &h) == GDP_OK) {
+        host_ = static_cast<float*>(h);
+    }
     GaussPy = new float***[layer];
     for (int o = 0; o < layer; ++o) {
         GaussPy[o] = new float**[S + 3];
@@ -215,6 +245,7 @@ inline void GaussPyramid_hip_mpi::SyncDevice() {
     host_dirty = false;
     host_current_ = true;
     fresh_ = band_live_ = false;  // the caller's contents: bands start from this rank's rows of them
+    arm_();
 }
 
 inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GPU), from the CURRENT `data`
@@ -227,6 +258,7 @@ inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GP
             check_(gdp_set_input_rows(band_, 0, (const int32_t* const*)(data + r0), nullptr), "GaussPyInit", band_);
     }
     host_dirty = false;
+    armed_ = false;  // every level is refilled on the device
     check_(gdp_init(full_, nullptr), "GaussPyInit", full_);
     is_initialized = true;
     fresh_ = true;

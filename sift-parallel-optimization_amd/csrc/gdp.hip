@@ -1999,9 +1999,10 @@ static void track_publish(TrackedMirror* t, void* host, size_t bytes, void* dma,
     const uintptr_t base = u / g_page_bytes * g_page_bytes;
     const uintptr_t end = (u + bytes + g_page_bytes - 1) / g_page_bytes * g_page_bytes;
     t->pages = (end - base) / g_page_bytes;
-    // a larger flag array when needed; the old one stays allocated (a handler on another thread may
-    // still read it), so a slot holds at most one array per size it has grown to
+    // a larger flag array when needed; the old one stays allocated and referenced (a handler on
+    // another thread may still read it): a slot keeps at most one array per size it has grown to
     if (t->written_cap < t->pages) {
+        if (t->written) g_track_retired->push_back(t->written);
         t->written = new std::atomic<unsigned char>[t->pages];
         t->written_cap = t->pages;
     }
@@ -2030,10 +2031,17 @@ int gdp_host_alloc_tracked(size_t bytes, void** host) try {
     void* dma = MAP_FAILED;
     void* cpu = MAP_FAILED;
     if (ftruncate(fd, (off_t)map) == 0) {
-        dma = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
-        cpu = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
+        dma = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        cpu = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     }
     close(fd);
+    if (dma != MAP_FAILED && cpu != MAP_FAILED) {
+        // huge pages where the kernel gives them to shared memory (fewer IOMMU translations for the
+        // DMA engines), then the pages faulted in through the DMA view before it is registered
+        (void)madvise(dma, map, MADV_HUGEPAGE);
+        (void)madvise(cpu, map, MADV_HUGEPAGE);
+        for (size_t off = 0; off < map; off += g_page_bytes) static_cast<volatile char*>(dma)[off] = 0;
+    }
     auto unmap = [&] {
         if (dma != MAP_FAILED) munmap(dma, map);
         if (cpu != MAP_FAILED) munmap(cpu, map);
@@ -2042,6 +2050,10 @@ int gdp_host_alloc_tracked(size_t bytes, void** host) try {
         unmap();
         return GDP_ERR_NOMEM;
     }
+    // like pinned memory, not inherited by fork()ed children (a shared mapping would otherwise let
+    // a child's writes reach this process's mirror)
+    (void)madvise(dma, map, MADV_DONTFORK);
+    (void)madvise(cpu, map, MADV_DONTFORK);
     const hipError_t e = hipHostRegister(dma, map, hipHostRegisterDefault);
     if (e != hipSuccess) {
         unmap();
