@@ -277,7 +277,9 @@ def dropin_call_cost(n=4096, calls=5):
     the default two-way GaussPy (mirror_host, write-tracked: the caller writes nothing, so only the
     in-place pass and the pyramid's download over PCIe, pipelined over row chunks), with the write
     tracking off (TrackWrites(false): the whole pyramid uploaded too, round 5's default) and with
-    mirror_host = false (the device pyramid is the state; no PCIe).  ADVICE r4 / VERDICT r5 item 2."""
+    mirror_host = false (the device pyramid is the state; no PCIe), and with the deferred download
+    (DeferDownload(true): nothing copied back until GaussPy is read; the read_all_* pair prices the
+    first full read after a call, eager against deferred).  ADVICE r4 / VERDICT r5 item 2."""
     import re
     import subprocess
 
@@ -285,12 +287,21 @@ def dropin_call_cost(n=4096, calls=5):
     if not os.path.exists(exe):
         return None
     out = {"n": n, "S": 2, "calls": calls,
-           "source": "examples/state_hip hip <n> 2 ones - [track:0 | mirror:0] dog time:<calls>"}
-    for key, ops in (("mirror_host_ms", []), ("mirror_untracked_ms", ["track:0"]), ("device_state_ms", ["mirror:0"])):
+           "source": "examples/state_hip hip <n> 2 ones - [track:0 | mirror:0 | defer:1] dog time:<calls>; "
+                     "[defer:1] dog read"}
+    for key, ops in (("mirror_host_ms", []), ("mirror_untracked_ms", ["track:0"]), ("device_state_ms", ["mirror:0"]),
+                     ("mirror_deferred_ms", ["defer:1"])):
         # one untimed call first (the mirror's copy streams and events are created on first use)
         r = subprocess.run([exe, "hip", str(n), "2", "ones", "-", *ops, "dog", f"time:{calls}"], capture_output=True,
                            text=True, timeout=120)
         m = re.search(r"([0-9.]+) ms per GenerateDoG", r.stderr)
+        out[key] = float(m.group(1)) if (r.returncode == 0 and m) else None
+    # reading every GaussPy float once after a call: eager mirror (already on the host) against the
+    # deferred one (each page fetched on first touch) — the difference is what deferral moves to the
+    # first read
+    for key, ops in (("read_all_eager_ms", ["dog", "read"]), ("read_all_deferred_ms", ["defer:1", "dog", "read"])):
+        r = subprocess.run([exe, "hip", str(n), "2", "ones", "-", *ops], capture_output=True, text=True, timeout=120)
+        m = re.search(r"read_ms=([0-9.]+)", r.stderr)
         out[key] = float(m.group(1)) if (r.returncode == 0 and m) else None
     pyr = 4 * 5 * pyramid_pixels(n, n, octaves_for(n))  # bytes each way per call
     if out.get("mirror_host_ms"):

@@ -13,6 +13,9 @@
 //   time:CALLS                                  time CALLS back-to-back GenerateDoG calls (stderr)
 //   track:0|1                                   TrackWrites (write-tracked mirror, default on)
 //   written                                     print `written=<bytes>` (the next upload) to stderr
+//   defer:0|1  stale                            DeferDownload; print `stale=<bytes>` to stderr
+//   read                                        read every GaussPy float once (fetches a deferred
+//                                               mirror page by page; prints `read_ms=` to stderr)
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -64,6 +67,19 @@ static int run(G& g, int n, int S, const char* path, int nops, char** ops, int a
         else if (op == "synchost") g.SyncHost();
         else if (op == "track") g.TrackWrites(num(1) != 0);
         else if (op == "written") std::fprintf(stderr, "written=%lld\n", g.written_bytes());
+        else if (op == "defer") std::fprintf(stderr, "deferring=%d\n", (int)g.DeferDownload(num(1) != 0));
+        else if (op == "stale") std::fprintf(stderr, "stale=%lld\n", g.stale_bytes());
+        else if (op == "read") {
+            auto t0 = std::chrono::high_resolution_clock::now();
+            double sum = 0;
+            int len = n;
+            for (int o = 0; o < gdp_octaves_for(n); ++o, len /= 2)
+                for (int sc = 0; sc < S + 3; ++sc)
+                    for (int r = 0; r < len; ++r)
+                        for (int c = 0; c < len; ++c) sum += g.GaussPy[o][sc][r][c];
+            auto t1 = std::chrono::high_resolution_clock::now();
+            std::fprintf(stderr, "read_ms=%.3f sum=%g\n", std::chrono::duration<double, std::milli>(t1 - t0).count(), sum);
+        }
         else if (op == "zero" || op == "neg" || op == "scale" || op == "set" || op == "reseat") {
             const int o = num(1), s = num(2), len = n >> o;
             if (op == "zero" || op == "neg") {
@@ -97,11 +113,17 @@ static int run(G& g, int n, int S, const char* path, int nops, char** ops, int a
     if (std::string(path) == "-") return 0;  // timing runs: no dump
     FILE* out = std::fopen(path, "wb");
     if (!out) return 3;
+    // each row through a local copy: fwrite may hand a long buffer straight to write(2), which a
+    // deferred GaussPy page would fail with EFAULT (the copy's CPU reads fetch it)
+    std::vector<float> row(n);
     int len = n;
     for (int o = 0; o < gdp_octaves_for(n); ++o, len /= 2)
         for (int sc = 0; sc < S + 3; ++sc)
-            for (int r = 0; r < len; ++r) std::fwrite(g.GaussPy[o][sc][r], sizeof(float), len, out);
-    std::fclose(out);
+            for (int r = 0; r < len; ++r) {
+                std::memcpy(row.data(), g.GaussPy[o][sc][r], sizeof(float) * len);
+                if (std::fwrite(row.data(), sizeof(float), len, out) != (size_t)len) return 3;
+            }
+    if (std::fclose(out) != 0) return 3;
     return 0;  // (reseated rows are leaked like the reference leaks `data`; the process ends here)
 }
 

@@ -60,7 +60,7 @@ inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
            "GenerateDoG_nomp_dynamic");
     fresh_ = false;
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG_nomp_dynamic");
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
 }
 
 inline void GaussPyramid_a512omp_hip::GenerateDoG() {
@@ -73,7 +73,7 @@ inline void GaussPyramid_a512omp_hip::GenerateDoG() {
     if (tiny < layer) check_(ctx_, gdp_dog_range(ctx_, tiny, layer, nullptr), "GenerateDoG");
     fresh_ = false;
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG");
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
 }
 
 class GaussPyramid_a512xp_hip : public GaussPyramid_hip {

@@ -37,6 +37,9 @@
 //    Writes that do not fault on the CPU (read(2) into GaussPy — EFAULT on a protected page —, or
 //    DMA into it) are not seen: call TrackWrites(false) first, and every call uploads the whole
 //    mirror as before (also the fallback when page protection is unavailable).
+//    DeferDownload(true) (opt-in): the copy back is deferred too — after a mutating call GaussPy's
+//    pages are inaccessible and the first access to one fetches its neighbourhood from the device
+//    (gdp_host_defer); main.cpp's loop then moves nothing over PCIe.  Reads see the same values.
 //  - mirror_host = false: the device pyramid is the state; GaussPy is refreshed only by
 //    SyncHost(), and host edits reach the device only through SyncDevice() — or set
 //    `host_dirty = true` after editing and the next mutating call uploads first (then clears it).
@@ -96,6 +99,20 @@ public:
         size_t b = 0;
         return track_ && armed_ && gdp_host_written_bytes(host_, &b) == GDP_OK ? (long long)b : -1;
     }
+    // Deferred download (opt-in, needs the write-tracked mirror): with mirror_host, a mutating call
+    // leaves GaussPy's pages inaccessible instead of copying the device pyramid back, and the first
+    // access to one has its neighbourhood fetched (gdp_host_defer).  A caller that does not read
+    // GaussPy between calls — main.cpp's timing loop (:66-73) — moves nothing over PCIe; one that
+    // reads it gets the same values as with the eager copy.  Off (the default), or for a caller
+    // that hands GaussPy to system calls (write(2) of a deferred page fails with EFAULT) or straight
+    // to HIP copies: call SyncHost() / DeferDownload(false) before those.  Returns whether it is on.
+    bool DeferDownload(bool on);
+    bool deferring() const { return defer_; }
+    // Bytes of GaussPy still to be fetched (inaccessible pages), or -1 when not deferring.
+    long long stale_bytes() const {
+        size_t b = 0;
+        return defer_ && gdp_host_deferred_stats(host_, &b, nullptr, nullptr) == GDP_OK ? (long long)b : -1;
+    }
     gdp_ctx* context() const { return ctx_; }
 
 protected:
@@ -110,6 +127,7 @@ protected:
     bool track_;  // host_ is write-tracked (gdp_host_track)
     bool armed_;  // the device pyramid equals host_ as of its last arming and the pages written
                   // since are recorded: the next mutating call may upload only those
+    bool defer_;  // DeferDownload: mutating calls end in gdp_host_defer instead of SyncHost
     bool rows_in_mirror_() const {  // every GaussPy row still where the constructor put it
         if (!host_) return false;
         for (int o = 0; o < layer; ++o)
@@ -121,7 +139,13 @@ protected:
             }
         return true;
     }
+    void keep_deferred_() {  // before a mutating call: a deferred GaussPy that the call will not
+        // defer again (mirror_host off, rows re-seated) is fetched now, while the device still
+        // holds what it shows
+        if (defer_ && !(mirror_host && rows_in_mirror_())) check_(ctx_, gdp_host_fetch(host_), "DeferDownload");
+    }
     void pull_host_() {  // before a mutating call: the caller's GaussPy is the state
+        keep_deferred_();
         const bool clean = armed_;
         armed_ = false;  // the call changes the device; SyncHost re-arms
         if (!(mirror_host || host_dirty)) return;
@@ -161,6 +185,14 @@ protected:
         check_(ctx_, mirrored_call_(), what);
         mirrored_done_();
     }
+    bool piped_() const { return mirror_host && !defer_ && rows_in_mirror_(); }  // the mirrored single call
+    void publish_() {  // after a mutating call with mirror_host: GaussPy shows the device pyramid
+        if (defer_ && rows_in_mirror_() && gdp_host_defer(ctx_, 0, host_) == GDP_OK) {
+            armed_ = true;  // pages fetched and then written are recorded from here on
+            return;
+        }
+        SyncHost();
+    }
     static void check_(gdp_ctx* c, int status, const char* what) {
         if (status != GDP_OK) {
             std::fprintf(stderr, "GaussPyramid_hip::%s failed: %s (%s)\n", what, gdp_status_string(status),
@@ -172,11 +204,13 @@ protected:
 
 inline GaussPyramid_hip::GaussPyramid_hip()
     : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), host_dirty(false), length(0), S(0),
-      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr), track_(false), armed_(false) {}
+      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr), track_(false), armed_(false),
+      defer_(false) {}
 
 inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device)
     : data(nullptr), GaussPy(nullptr), initialized(false), mirror_host(true), host_dirty(false), length(len), S(S_),
-      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr), track_(false), armed_(false) {
+      layer(0), filter(nullptr), ctx_(nullptr), fresh_(false), host_(nullptr), track_(false), armed_(false),
+      defer_(false) {
     data = new int*[len];
     for (int i = 0; i < len; ++i) {
         data[i] = new int[len];
@@ -230,15 +264,22 @@ inline void GaussPyramid_hip::SyncDevice() {  // the inverse: the whole mirror, 
 
 inline void GaussPyramid_hip::TrackWrites(bool on) {
     if (!on && track_) {
-        check_(ctx_, gdp_host_untrack(host_), "TrackWrites");  // every page writable again
-        track_ = armed_ = false;
+        check_(ctx_, gdp_host_untrack(host_), "TrackWrites");  // fetched if deferred; every page writable again
+        track_ = armed_ = defer_ = false;
     } else if (on && !track_ && host_) {
         // armed by the next SyncHost (every mutating call with mirror_host ends in one)
         track_ = gdp_host_track(host_, gdp_image_floats(ctx_) * sizeof(float)) == GDP_OK;
     }
 }
 
+inline bool GaussPyramid_hip::DeferDownload(bool on) {
+    if (!on && defer_) check_(ctx_, gdp_host_fetch(host_), "DeferDownload");  // GaussPy complete again
+    defer_ = on && track_ && host_;  // takes effect from the next mutating call
+    return defer_;
+}
+
 inline void GaussPyramid_hip::GaussPyInit() {  // :60-87, from the CURRENT `data` (:80)
+    keep_deferred_();
     armed_ = false;  // every level is refilled on the device
     if (mirror_host || host_dirty)
         check_(ctx_, gdp_set_input_rows(ctx_, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
@@ -246,18 +287,18 @@ inline void GaussPyramid_hip::GaussPyInit() {  // :60-87, from the CURRENT `data
     check_(ctx_, gdp_init(ctx_, nullptr), "GaussPyInit");
     initialized = true;
     fresh_ = true;
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
 }
 
 inline void GaussPyramid_hip::GaussFilter(int theLayer) {
     pull_host_();
     check_(ctx_, gdp_gauss_octave(ctx_, theLayer, nullptr), "GaussFilter");
     fresh_ = false;
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
 }
 
 inline void GaussPyramid_hip::GenerateDoG() {
-    if (mirror_host && rows_in_mirror_()) {
+    if (piped_()) {
         // GaussPy mirrored in the pinned device-layout buffer: upload (only the pages written since
         // the last call when tracked), in-place pass and download in one call, pipelined over row
         // chunks
@@ -270,13 +311,13 @@ inline void GaussPyramid_hip::GenerateDoG() {
     check_(ctx_, fresh_ ? gdp_build(ctx_, nullptr) : gdp_generate_dog(ctx_, nullptr), "GenerateDoG");
     fresh_ = false;
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG");
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
 }
 
 inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
     // switching centres selects the other device tap table (no drain, no re-upload after the
     // first call); both calls below are ordered on the context's stream
-    const bool piped = mirror_host && rows_in_mirror_();  // see GenerateDoG
+    const bool piped = piped_();  // see GenerateDoG
     if (!piped) pull_host_();
     check_(ctx_, gdp_set_window_centre(ctx_, GDP_CENTRE_INTLEN), "GenerateDoG_mpi");
     if (piped) {
@@ -291,7 +332,7 @@ inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
     check_(ctx_, rc, "GenerateDoG_mpi");
     fresh_ = false;
     check_(ctx_, gdp_sync(ctx_), "GenerateDoG_mpi");
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
 }
 
 inline void GaussPyramid_hip::output() {  // :89-104

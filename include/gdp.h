@@ -298,6 +298,27 @@ int gdp_host_arm(void* host);
 int gdp_host_written_bytes(const void* host, size_t* bytes);
 int gdp_upload_image_written(gdp_ctx* ctx, int b, const float* host);
 int gdp_generate_dog_mirrored_written(gdp_ctx* ctx, int b, float* host);
+/* Deferred download (opt-in; the drop-in's GaussPyramid_hip::DeferDownload).  gdp_host_defer: the
+ * caller asserts that image b's device pyramid of `ctx` is now NEWER than the tracked
+ * gdp_host_alloc_tracked buffer `host` (at most gdp_image_floats floats), instead of downloading
+ * it: every page of the CPU view becomes inaccessible, and the first CPU access to one (read or
+ * write) faults, has a block of pages around it copied from the device — 64 pages, doubling to 8192
+ * while the faults walk forward — on the context's stream by a libgdp helper thread, and arms them
+ * (a write then faults once more and is recorded, as above).  Not blocking: the fetches are ordered
+ * after the work queued on the context's stream.  Host writes not uploaded yet are discarded (the
+ * device copy is declared the newer one).  gdp_host_fetch completes a deferred buffer now (every
+ * inaccessible page fetched; gdp_download_image_raw(b, host) of the whole image ends the deferral
+ * by overwriting it).  Every libgdp entry taking caller host memory completes deferred buffers
+ * first, and gdp_destroy completes those deferred to its context; gdp_host_untrack / gdp_host_arm
+ * of a deferred buffer complete it first.  gdp_host_deferred_stats: inaccessible bytes (whole
+ * pages) and the bytes / copies fetched since the last gdp_host_defer (any argument may be NULL).
+ * Limits on top of write tracking's: a system call READING a deferred page (write(2), send(2) from
+ * it) fails with EFAULT, and a fault while the faulting thread holds a HIP runtime lock (the
+ * buffer's CPU view handed straight to a HIP copy) cannot be served — call gdp_host_fetch before
+ * either.  GDP_ERR_STATE: `host` is not a tracked gdp_host_alloc_tracked buffer. */
+int gdp_host_defer(gdp_ctx* ctx, int b, void* host);
+int gdp_host_fetch(void* host);
+int gdp_host_deferred_stats(const void* host, size_t* stale_bytes, size_t* fetched_bytes, uint64_t* fetches);
 /* Order-independent 64-bit checksum of image b's pyramid (blocking): the sum, mod 2^64, over
  * every word of every level of splitmix64_fin(idx * 0x9E3779B97F4A7C15 + (o*64+s) *
  * 0xD1B54A32D192ED03 + float_bits), idx = global_row * cols + col.  Row-band checksums add up

@@ -104,6 +104,10 @@ SIGNATURES = {
     "gdp_host_untrack": (_c_int, [_p]),
     "gdp_host_arm": (_c_int, [_p]),
     "gdp_host_written_bytes": (_c_int, [_p, ctypes.POINTER(ctypes.c_size_t)]),
+    "gdp_host_defer": (_c_int, [_p, _c_int, _p]),
+    "gdp_host_fetch": (_c_int, [_p]),
+    "gdp_host_deferred_stats": (_c_int, [_p, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_uint64)]),
     "gdp_upload_image_written": (_c_int, [_p, _c_int, _p]),
     "gdp_generate_dog_mirrored_written": (_c_int, [_p, _c_int, _p]),
     "gdp_checksum": (_c_int, [_p, _c_int, ctypes.POINTER(ctypes.c_uint64)]),

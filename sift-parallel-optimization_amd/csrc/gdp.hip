@@ -34,8 +34,11 @@
 #include <mutex>
 #include <vector>
 
+#include <linux/futex.h>
+#include <sched.h>
 #include <signal.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include "gdp.h"
@@ -532,7 +535,8 @@ hipError_t launch_conv_sweep_t(gdp_ctx* c, unsigned units, hipStream_t st) {
 template <int L, int T, int W>
 hipError_t launch_conv_blk_t(gdp_ctx* c, unsigned units, hipStream_t st) {
     // the default pacing (vmcnt(2)) compiled in for the 16-wave tiles; any other pace, and the
-    // 8-wave tiles, read it at run time
+    // 8-wave tiles, read it at run time.  (Round 6, every pace compiled in for S = 2 and measured
+    // alternated twice on c2 / c4 / c5: all within 0.7 % — conv_pace_ab_r06m.log.)
     auto k = (W == 16 && c->geom.conv_pace == 2) ? k_conv_blk<L, T, W, kBkHaloLanes, 2>
                                                  : k_conv_blk<L, T, W, kBkHaloLanes, kPaceRuntime>;
     const unsigned grid = (c->conv_order & 1) ? (units + 7u) / 8u * 8u : units;
@@ -590,6 +594,32 @@ static int abi_exception(const gdp_ctx* c, int code, const char* what) noexcept 
     catch (const std::bad_alloc&) { return abi_exception((ctx), GDP_ERR_NOMEM, "host allocation failed (std::bad_alloc)"); } \
     catch (const std::exception& e_) { return abi_exception((ctx), GDP_ERR_INTERNAL, e_.what()); }         \
     catch (...) { return abi_exception((ctx), GDP_ERR_INTERNAL, "unknown C++ exception"); }
+
+// Deferred mirrors overlapping the caller host memory an entry is given are completed first: no
+// libgdp copy may fault on a stale page (gdp_track.inc).  `ranges(f)` calls f(ptr, bytes) for
+// each host range the entry touches; a registry lock and one walk over its slots when nothing is
+// deferred.
+static size_t packed_pyramid_bytes(const gdp_ctx* c) {  // gdp_download_pyramid's layout
+    size_t n = 0;
+    for (int o = 0; o < c->geom.O; ++o) n += (size_t)c->geom.oct[o].rows * c->geom.oct[o].cols * c->geom.L;
+    return n * 4;
+}
+template <class F>
+static int settle_deferred(gdp_ctx* c, const char* what, F&& ranges) {
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    if (!track_any_deferred()) return GDP_OK;
+    int rc = GDP_OK;
+    ranges([&](const void* p, size_t n) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        if (p && n && track_settle_overlap(a, a + n) != GDP_OK) rc = GDP_ERR_HIP;
+    });
+    return rc == GDP_OK ? GDP_OK : c->status(rc, "%s: completing a deferred host mirror failed", what);
+}
+#define GDP_SETTLE(c, what, ...)                                          \
+    do {                                                                  \
+        const int settle_rc_ = settle_deferred((c), (what), __VA_ARGS__); \
+        if (settle_rc_ != GDP_OK) return settle_rc_;                      \
+    } while (0)
 
 extern "C" {
 
@@ -1081,6 +1111,11 @@ void gdp_destroy(gdp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    {
+        // host mirrors deferred to this context keep their contents: fetched now
+        std::lock_guard<std::mutex> lk(g_track_mu);
+        (void)track_settle_all(c);
+    }
     if (c->d_geom) (void)hipFree(c->d_geom);
     for (float* t : c->d_taps_mode)
         if (t) (void)hipFree(t);
@@ -1171,10 +1206,12 @@ int bind_input(gdp_ctx* c, const void* base, size_t pitch, size_t image_stride, 
 }  // namespace
 
 int gdp_set_input_host(gdp_ctx* c, int b, const int32_t* base, size_t pitch, void* stream) try {
+    if (c) GDP_SETTLE(c, "gdp_set_input_host", [&](auto&& f) { f(base, pitch * 4 * (size_t)c->geom.in_rows); });
     return upload_input(c, b, base, pitch, GDP_INPUT_I32, stream, "gdp_set_input_host");
 } GDP_ABI_CATCH(c)
 
 int gdp_set_input_host_u8(gdp_ctx* c, int b, const uint8_t* base, size_t pitch, void* stream) try {
+    if (c) GDP_SETTLE(c, "gdp_set_input_host_u8", [&](auto&& f) { f(base, pitch * (size_t)c->geom.in_rows); });
     return upload_input(c, b, base, pitch, GDP_INPUT_U8, stream, "gdp_set_input_host_u8");
 } GDP_ABI_CATCH(c)
 
@@ -1191,6 +1228,7 @@ int gdp_set_input_rows(gdp_ctx* c, int b, const int32_t* const* rows, void* stre
         if (!rows[r]) return c->status(GDP_ERR_ARG, "gdp_set_input_rows: null row %zu", r);
     if (W * R == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_set_input_rows", [&](auto&& f) { for (size_t r = 0; r < R; ++r) f(rows[r], W * 4); });
     hipStream_t st = c->pick(stream);
     // The rows are gathered into the double-buffered pinned staging (the mirror of
     // stage_download): the host gathers batch k into one half while batch k-1's 2-D copy runs.
@@ -1510,6 +1548,7 @@ const float* gdp_device_level(const gdp_ctx* c, int b, int o, int s) {
 int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) try {
     if (!valid_level(c, b, o, s) || !host) return c ? c->status(GDP_ERR_ARG, "gdp_download_level: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_download_level", [&](auto&& f) { f(host, (size_t)c->geom.oct[o].rows * c->geom.oct[o].cols * 4); });
     const OctGeom& og = c->geom.oct[o];
     GDP_HIP(c, hipMemcpyAsync(host, gdp_device_level(c, b, o, s), (size_t)og.rows * og.cols * 4, hipMemcpyDeviceToHost,
                               c->stream));
@@ -1631,6 +1670,7 @@ int gdp_download_level_rows(gdp_ctx* c, int b, int o, int s, float* const* rows)
     const OctGeom& og = c->geom.oct[o];
     if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_download_level_rows", [&](auto&& f) { for (int r = 0; r < og.rows; ++r) f(rows[r], (size_t)og.cols * 4); });
     return stage_download(c, {{gdp_device_level(c, b, o, s), (size_t)og.cols, (size_t)og.rows, rows, 0}});
 } GDP_ABI_CATCH(c)
 
@@ -1638,6 +1678,11 @@ int gdp_download_pyramid_rows(gdp_ctx* c, int b, float* const* const* const* py)
     if (!c || !py || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid_rows: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_download_pyramid_rows", [&](auto&& f) {
+        for (int o = 0; o < c->geom.O; ++o)
+            for (int s = 0; s < c->geom.L && py[o]; ++s)
+                for (int r = 0; r < c->geom.oct[o].rows && py[o][s]; ++r) f(py[o][s][r], (size_t)c->geom.oct[o].cols * 4);
+    });
     const Geom& g = c->geom;
     std::vector<StagePiece> pieces;
     for (int o = 0; o < g.O; ++o) {
@@ -1655,6 +1700,7 @@ int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int
         return c ? c->status(GDP_ERR_ARG, "gdp_download_level_range: bad argument") : GDP_ERR_ARG;
     if (nrows == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_download_level_range", [&](auto&& f) { f(host, (size_t)nrows * c->geom.oct[o].cols * 4); });
     const OctGeom& og = c->geom.oct[o];
     GDP_HIP(c, hipMemcpyAsync(host, gdp_device_level(c, b, o, s) + (size_t)first_row * og.cols,
                               (size_t)nrows * og.cols * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1665,6 +1711,7 @@ int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int
 int gdp_download_pyramid(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_download_pyramid: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_download_pyramid", [&](auto&& f) { f(host, packed_pyramid_bytes(c)); });
     size_t off = 0;
     for (int o = 0; o < c->geom.O; ++o) {
         const OctGeom& og = c->geom.oct[o];
@@ -1679,6 +1726,7 @@ int gdp_download_pyramid(gdp_ctx* c, int b, float* host) try {
 int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_upload_pyramid: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_upload_pyramid", [&](auto&& f) { f(host, packed_pyramid_bytes(c)); });
     size_t off = 0;
     for (int o = 0; o < c->geom.O; ++o) {
         const OctGeom& og = c->geom.oct[o];
@@ -1765,6 +1813,7 @@ int gdp_upload_level(gdp_ctx* c, int b, int o, int s, const float* host) try {
     const OctGeom& og = c->geom.oct[o];
     if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_upload_level", [&](auto&& f) { f(host, (size_t)og.rows * og.cols * 4); });
     GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), host, (size_t)og.rows * og.cols * 4,
                               hipMemcpyHostToDevice, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
@@ -1776,6 +1825,7 @@ int gdp_upload_level_rows(gdp_ctx* c, int b, int o, int s, const float* const* r
     const OctGeom& og = c->geom.oct[o];
     if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_upload_level_rows", [&](auto&& f) { for (int r = 0; r < og.rows; ++r) f(rows[r], (size_t)og.cols * 4); });
     return stage_upload(c, {{const_cast<float*>(gdp_device_level(c, b, o, s)), (size_t)og.cols, (size_t)og.rows, rows}});
 } GDP_ABI_CATCH(c)
 
@@ -1783,6 +1833,11 @@ int gdp_upload_pyramid_rows(gdp_ctx* c, int b, const float* const* const* const*
     if (!c || !py || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_upload_pyramid_rows: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_upload_pyramid_rows", [&](auto&& f) {
+        for (int o = 0; o < c->geom.O; ++o)
+            for (int s = 0; s < c->geom.L && py[o]; ++s)
+                for (int r = 0; r < c->geom.oct[o].rows && py[o][s]; ++r) f(py[o][s][r], (size_t)c->geom.oct[o].cols * 4);
+    });
     const Geom& g = c->geom;
     std::vector<UpPiece> pieces;
     for (int o = 0; o < g.O; ++o) {
@@ -1801,6 +1856,7 @@ int gdp_upload_image_raw(gdp_ctx* c, int b, const float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_upload_image_raw: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_upload_image_raw", [&](auto&& f) { f(host, (size_t)c->img_floats * 4); });
     GDP_HIP(c, hipMemcpyAsync(c->d_out + (size_t)b * c->geom.pyr_stride, track_dma_ptr(host), (size_t)c->img_floats * 4,
                               hipMemcpyHostToDevice, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
@@ -1811,6 +1867,7 @@ int gdp_get_taps(gdp_ctx* c, int axis, int o, int s, float* host) try {
     if (!c || !host || o < 0 || o >= c->geom.O || s < 0 || s >= c->geom.L || (axis != 0 && axis != 1))
         return c ? c->status(GDP_ERR_ARG, "gdp_get_taps: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    GDP_SETTLE(c, "gdp_get_taps", [&](auto&& f) { f(host, (size_t)(axis == 0 ? c->geom.oct[o].cols : (c->geom.H >> o)) * 4); });
     const OctGeom& og = c->geom.oct[o];
     const int n = axis == 0 ? og.cols : (c->geom.H >> o);
     const long long off = axis == 0 ? og.ctap + (long long)s * og.ctap_stride : og.rtap + (long long)s * og.rtap_stride;
@@ -1872,14 +1929,45 @@ void gdp_host_free(void* host) {
 
 size_t gdp_image_floats(const gdp_ctx* c) { return c ? (size_t)c->img_floats : 0; }
 
+// A whole-image download into `host` is about to replace a deferred mirror's contents: true when
+// it covers the mirror exactly (its stale pages then end as clean — track_undefer after the copy);
+// any other deferred mirror is completed first.
+static bool download_covers_deferred(gdp_ctx* c, const void* host, int* rc) {
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    const TrackedMirror* t = track_find(host);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(host);
+    const size_t n = (size_t)c->img_floats * 4;
+    if (t && t->stale && t->user_bytes <= n) {
+        *rc = GDP_OK;
+        for (TrackedMirror& u : g_tracked) {
+            const uintptr_t b = u.base.load(std::memory_order_relaxed);
+            if (&u != t && b && u.stale && a < b + u.bytes.load(std::memory_order_relaxed) && a + n > b &&
+                track_settle(u) != GDP_OK)
+                *rc = GDP_ERR_HIP;
+        }
+        return true;
+    }
+    *rc = track_settle_overlap(a, a + n);
+    return false;
+}
+static int finish_download(gdp_ctx* c, const void* host, bool covers) {
+    if (!covers) return GDP_OK;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    TrackedMirror* t = track_find(host);
+    return t && track_undefer(*t) != GDP_OK ? c->status(GDP_ERR_STATE, "mprotect refused arming a downloaded mirror") : GDP_OK;
+}
+
 int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_download_image_raw: bad argument") : GDP_ERR_ARG;
     GDP_HIP(c, hipSetDevice(c->device));
+    int rc = GDP_OK;
+    const bool covers = download_covers_deferred(c, host, &rc);
+    if (rc != GDP_OK) return c->status(rc, "gdp_download_image_raw: completing a deferred host mirror failed");
     GDP_HIP(c, hipMemcpyAsync(track_dma_ptr(host), c->d_out + (size_t)b * c->geom.pyr_stride, (size_t)c->img_floats * 4,
                               hipMemcpyDeviceToHost, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
-    return GDP_OK;
+    return finish_download(c, host, covers);
 } GDP_ABI_CATCH(c)
 
 // GenerateDoG on a HOST pyramid (the drop-in classes' mirrored GaussPy, GuassDePyramid.h:16,
@@ -1971,6 +2059,7 @@ static int generate_dog_mirrored(gdp_ctx* c, int b, float* host, const std::vect
 int gdp_generate_dog_mirrored(gdp_ctx* c, int b, float* host) try {
     if (!c || !host || b < 0 || b >= c->geom.batch)
         return c ? c->status(GDP_ERR_ARG, "gdp_generate_dog_mirrored: bad argument") : GDP_ERR_ARG;
+    GDP_SETTLE(c, "gdp_generate_dog_mirrored", [&](auto&& f) { f(host, (size_t)c->img_floats * 4); });  // the whole host image is the input
     return generate_dog_mirrored(c, b, track_dma_ptr(host), nullptr);
 } GDP_ABI_CATCH(c)
 
@@ -2092,6 +2181,7 @@ int gdp_host_untrack(void* host) try {
     std::lock_guard<std::mutex> lk(g_track_mu);
     TrackedMirror* t = host ? track_find(host) : nullptr;
     if (!t || !t->tracking) return GDP_ERR_ARG;
+    if (track_settle(*t) != GDP_OK) return GDP_ERR_HIP;  // a deferred mirror is completed first
     const uintptr_t base = t->base.load(std::memory_order_relaxed);
     const int rc = mprotect(reinterpret_cast<void*>(base), t->bytes.load(std::memory_order_relaxed), PROT_READ | PROT_WRITE) == 0
                        ? GDP_OK
@@ -2110,6 +2200,7 @@ int gdp_host_arm(void* host) try {
     // already armed: every page not written since is still protected, so only the written ones
     // are protected again (no walk over the whole range)
     if (t->armed) return track_rearm(*t, track_written_runs(*t), false);
+    if (track_settle(*t) != GDP_OK) return GDP_ERR_HIP;  // (arming all: stale pages fetched first)
     return track_rearm(*t, {}, true);
 } GDP_ABI_CATCH(nullptr)
 
@@ -2123,7 +2214,7 @@ int gdp_host_written_bytes(const void* host, size_t* bytes) try {
     const uintptr_t u0 = reinterpret_cast<uintptr_t>(t->user), u1 = u0 + t->user_bytes;
     size_t n = 0;
     for (size_t p = 0; p < t->pages; ++p)
-        if (t->written[p].load(std::memory_order_relaxed)) {
+        if (t->written[p].load(std::memory_order_relaxed) == kPageWritten) {
             const uintptr_t lo = std::max<uintptr_t>(u0, b + p * g_page_bytes);
             const uintptr_t hi = std::min<uintptr_t>(u1, b + (p + 1) * g_page_bytes);
             n += hi > lo ? hi - lo : 0;
@@ -2163,6 +2254,9 @@ int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
     {
         std::lock_guard<std::mutex> lk(g_track_mu);
         t = track_for_image(c, host, &runs, &partial);
+        // the written runs never cover a stale page; a whole upload needs every page current
+        if (!partial && track_settle_overlap(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(host) + (size_t)c->img_floats * 4) != GDP_OK)
+            return c->status(GDP_ERR_HIP, "gdp_upload_image_written: completing a deferred host mirror failed");
     }
     const char* src = static_cast<const char*>(track_dma_ptr(static_cast<const void*>(host)));
     GDP_HIP(c, hipSetDevice(c->device));
@@ -2189,6 +2283,9 @@ int gdp_generate_dog_mirrored_written(gdp_ctx* c, int b, float* host) try {
     {
         std::lock_guard<std::mutex> lk(g_track_mu);
         t = track_for_image(c, host, &runs, &partial);
+        // (as gdp_upload_image_written; the download at the end replaces every page)
+        if (!partial && track_settle_overlap(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(host) + (size_t)c->img_floats * 4) != GDP_OK)
+            return c->status(GDP_ERR_HIP, "gdp_generate_dog_mirrored_written: completing a deferred host mirror failed");
     }
     const int rc = generate_dog_mirrored(c, b, track_dma_ptr(host), partial ? &runs : nullptr);
     std::lock_guard<std::mutex> lk(g_track_mu);
@@ -2196,10 +2293,85 @@ int gdp_generate_dog_mirrored_written(gdp_ctx* c, int b, float* host) try {
         if (t) t->armed = false;  // the device may hold a partial result: the next call uploads all
         return rc;
     }
+    if (t && track_undefer(*t) != GDP_OK)
+        return c->status(GDP_ERR_STATE, "gdp_generate_dog_mirrored_written: mprotect refused arming the mirror");
     if (t && track_rearm(*t, runs, !partial) != GDP_OK)
         return c->status(GDP_ERR_STATE, "gdp_generate_dog_mirrored_written: mprotect refused re-arming the mirror");
     return GDP_OK;
 } GDP_ABI_CATCH(c)
+
+// ---- deferred download (gdp_track.inc) ----
+int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
+    if (!c || !host || b < 0 || b >= c->geom.batch)
+        return c ? c->status(GDP_ERR_ARG, "gdp_host_defer: bad argument") : GDP_ERR_ARG;
+    const size_t img_bytes = (size_t)c->img_floats * 4;
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    TrackedMirror* t = track_find(host);
+    if (!t || !t->tracking || !t->dma)
+        return c->status(GDP_ERR_STATE, "gdp_host_defer: not a write-tracked gdp_host_alloc_tracked buffer");
+    if (t->user_bytes > img_bytes)
+        return c->status(GDP_ERR_ARG, "gdp_host_defer: the buffer (%zu bytes) is larger than the image (%zu)", t->user_bytes,
+                         img_bytes);
+    const char* src = reinterpret_cast<const char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
+    // stale pages of ANOTHER source are fetched first (they are older than this image only if the
+    // caller says so for every page — it does not: only for the image it names)
+    if (t->stale && (t->src_ctx != c || t->src != src) && track_settle(*t) != GDP_OK)
+        return c->status(GDP_ERR_HIP, "gdp_host_defer: completing the previous deferral failed");
+    if (!g_fetch_worker.exchange(true)) std::thread(track_fetch_worker).detach();
+    state_lock();
+    const uintptr_t base = t->base.load(std::memory_order_relaxed);
+    int rc = GDP_OK;
+    for (size_t p = 0; p < t->pages;) {  // every page not stale yet: no access
+        if (t->written[p].load(std::memory_order_relaxed) == kPageStale) {
+            ++p;
+            continue;
+        }
+        size_t q = p + 1;
+        while (q < t->pages && t->written[q].load(std::memory_order_relaxed) != kPageStale) ++q;
+        if (mprotect(reinterpret_cast<void*>(base + p * g_page_bytes), (q - p) * g_page_bytes, PROT_NONE) != 0) {
+            rc = GDP_ERR_STATE;
+            break;
+        }
+        for (size_t k = p; k < q; ++k) t->written[k].store(kPageStale, std::memory_order_relaxed);
+        t->stale += q - p;
+        p = q;
+    }
+    t->src_ctx = c;
+    t->src = src;
+    t->src_bytes = img_bytes;
+    t->src_device = c->device;
+    t->src_stream = c->stream;
+    t->ra_next = t->ra_len = 0;
+    t->fetched_bytes = 0;
+    t->fetches = 0;
+    t->armed = rc == GDP_OK;  // no written page is pending: a record exists (nothing written yet)
+    state_unlock();
+    if (rc != GDP_OK) {
+        // the mirror is in a mixed state: complete it and give up tracking
+        (void)track_settle(*t);
+        return c->status(GDP_ERR_STATE, "gdp_host_defer: mprotect refused");
+    }
+    return GDP_OK;
+} GDP_ABI_CATCH(c)
+
+int gdp_host_fetch(void* host) try {
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    TrackedMirror* t = host ? track_find(host) : nullptr;
+    if (!t) return GDP_ERR_ARG;
+    return track_settle(*t);
+} GDP_ABI_CATCH(nullptr)
+
+int gdp_host_deferred_stats(const void* host, size_t* stale_bytes, size_t* fetched_bytes, uint64_t* fetches) try {
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    const TrackedMirror* t = host ? track_find(host) : nullptr;
+    if (!t) return GDP_ERR_ARG;
+    state_lock();
+    if (stale_bytes) *stale_bytes = t->stale * g_page_bytes;
+    if (fetched_bytes) *fetched_bytes = t->fetched_bytes;
+    if (fetches) *fetches = t->fetches;
+    state_unlock();
+    return GDP_OK;
+} GDP_ABI_CATCH(nullptr)
 
 int gdp_checksum(gdp_ctx* c, int b, uint64_t* out) try {
     if (!c || !out || b < 0 || b >= c->geom.batch) return c ? c->status(GDP_ERR_ARG, "gdp_checksum: bad argument") : GDP_ERR_ARG;

@@ -90,8 +90,8 @@ class _Replay:
             self.host[:] = self.pyr
         elif f[0] == "data":
             self.img[int(f[1]), int(f[2])] = int(f[3])
-        elif f[0] in ("reseat", "track", "written"):
-            pass  # same contents, another address / the upload strategy / a report
+        elif f[0] in ("reseat", "track", "written", "defer", "stale", "read"):
+            pass  # same contents, another address / the upload or download strategy / a report
         else:
             lv = self._lv(self.host, int(f[1]), int(f[2]))
             if f[0] == "zero":
@@ -115,7 +115,7 @@ def _assert_same_nan(got, want, what):
     _assert_same(g.view(np.float32), w.view(np.float32), what)
 
 
-def _run(oracle, tmp_path, cls, n, S, spec, ops):
+def _run(oracle, tmp_path, cls, n, S, spec, ops, want_stale=False):
     if not os.path.exists(EXE):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples")], check=True)
     out = tmp_path / "state.f32"
@@ -125,6 +125,9 @@ def _run(oracle, tmp_path, cls, n, S, spec, ops):
     for op in ops:
         rp.apply(op)
     _assert_same(np.fromfile(out, dtype=np.float32), rp.host, (cls, n, S, ops))
+    if want_stale:
+        return ([int(x) for x in re.findall(r"written=(-?\d+)", r.stderr)],
+                [int(x) for x in re.findall(r"stale=(-?\d+)", r.stderr)])
     return [int(x) for x in re.findall(r"written=(-?\d+)", r.stderr)]
 
 
@@ -506,13 +509,112 @@ def test_tracked_mirror_uploads_only_written_pages(pkg, oracle):
             L.gdp_host_free(hptr)
 
 
-def test_cpp_class_random_edit_sequences_with_write_tracking(oracle, tmp_path):
+def test_deferred_mirror_fetches_on_first_touch(pkg, oracle):
+    """gdp_host_defer: the device pyramid is declared newer than the tracked mirror; every page of
+    its CPU view is inaccessible until touched, and a touch fetches a block around it (64 pages,
+    doubling while the faults walk forward).  Random reads through numpy equal the device copy
+    while only part of the mirror has moved; a write is recorded as one page; a sequential pass
+    fetches the rest in few, growing copies; an unrelated download leaves the deferral alone;
+    gdp_destroy of the source context completes the mirror; buffers that cannot defer are refused."""
+    import ctypes
+
+    L = pkg.lib()
+    page = os.sysconf("SC_PAGESIZE")
+    H = W = 2048
+    S = 2
+    size_t = ctypes.c_size_t
+    with pkg.PyramidContext(H, W, S=S) as a:
+        n = L.gdp_image_floats(a._ctx)
+        a.set_input(oracle.lcg_image(H, W, 91), 0)
+        a.build()
+        a.sync()
+        ref = np.empty(n, np.float32)
+        assert L.gdp_download_image_raw(a._ctx, 0, ref.ctypes.data_as(ctypes.c_void_p)) == 0
+        pinned = ctypes.c_void_p()
+        assert L.gdp_host_alloc(n * 4, ctypes.byref(pinned)) == 0
+        try:
+            assert L.gdp_host_defer(a._ctx, 0, pinned) == 3  # not a tracked alias: refused
+        finally:
+            L.gdp_host_free(pinned)
+        hptr = ctypes.c_void_p()
+        assert L.gdp_host_alloc_tracked(n * 4, ctypes.byref(hptr)) == 0
+        try:
+            host = np.ctypeslib.as_array(ctypes.cast(hptr, ctypes.POINTER(ctypes.c_float)), shape=(n,))
+            stale, fetched, fetches = size_t(), size_t(), ctypes.c_uint64()
+
+            def stats():
+                assert L.gdp_host_deferred_stats(hptr, ctypes.byref(stale), ctypes.byref(fetched),
+                                                 ctypes.byref(fetches)) == 0
+                return stale.value, fetched.value, fetches.value
+
+            assert L.gdp_host_defer(a._ctx, 0, hptr) == 0
+            full = stats()[0]
+            assert full >= n * 4 and full % page == 0, full
+            rng = np.random.default_rng(5)
+            idx = np.sort(rng.integers(0, n, 40))
+            _assert_same(host[idx], ref[idx], "random reads of a deferred mirror")
+            st, fb, nf = stats()
+            assert 0 < nf <= 40 and 0 < fb < full // 2 and full - page < st + fb <= full, (st, fb, nf)
+            # a download into other memory does not touch the deferral
+            got = np.empty(n, np.float32)
+            assert L.gdp_download_image_raw(a._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            assert stats()[0] == st
+            k = int(idx[3]) + 1
+            host[k] = np.float32(-7.0)  # a fetched page: one more fault, recorded
+            ref[k] = np.float32(-7.0)
+            written = size_t()
+            assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 0 and written.value == page
+            _assert_same(host, ref, "whole deferred mirror after the touches")  # fetches the rest
+            st, fb, nf = stats()
+            # (a sequential copy stops at each block the random reads fetched: at most two more each)
+            assert st == 0 and nf <= 2 * 40 + 40, (st, fb, nf)
+            # the written page goes up with the next written-page upload; a pass and a new deferral
+            assert L.gdp_upload_image_written(a._ctx, 0, hptr) == 0
+            assert L.gdp_download_image_raw(a._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            _assert_same(got, ref, "device after the written-page upload")
+            assert L.gdp_generate_dog(a._ctx, None) == 0
+            assert L.gdp_host_defer(a._ctx, 0, hptr) == 0  # not blocking: fetches queue behind the pass
+            assert L.gdp_download_image_raw(a._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
+            seen = np.empty(n, np.float32)
+            for lo in range(0, n, 1 << 20):  # sequential reads: few, growing copies
+                seen[lo:lo + (1 << 20)] = host[lo:lo + (1 << 20)]
+            _assert_same(seen, got, "sequential reads of the deferred pass result")
+            st, fb, nf = stats()
+            assert st == 0 and nf <= 32, (st, fb, nf)
+            with pkg.PyramidContext(H, W, S=S) as b:  # source context destroyed while deferred
+                b.set_input(oracle.lcg_image(H, W, 92), 0)
+                b.build()
+                b.sync()
+                want = np.empty(n, np.float32)
+                assert L.gdp_download_image_raw(b._ctx, 0, want.ctypes.data_as(ctypes.c_void_p)) == 0
+                assert L.gdp_host_defer(b._ctx, 0, hptr) == 0
+            assert stats()[0] == 0
+            _assert_same(host, want, "mirror completed by gdp_destroy of its source")
+            assert L.gdp_host_defer(a._ctx, 0, hptr) == 0
+            assert L.gdp_host_fetch(hptr) == 0 and stats()[0] == 0
+            _assert_same(host, got, "gdp_host_fetch")
+            assert L.gdp_host_defer(a._ctx, 0, hptr) == 0
+            assert L.gdp_download_image_raw(a._ctx, 0, hptr) == 0  # whole download ends the deferral
+            assert stats()[0] == 0 and stats()[2] == 0
+            _assert_same(host, got, "download over a deferred mirror")
+            assert L.gdp_host_defer(a._ctx, 0, hptr) == 0
+            assert L.gdp_host_untrack(hptr) == 0  # completes it first
+            _assert_same(host, got, "untrack of a deferred mirror")
+            assert L.gdp_host_defer(a._ctx, 0, hptr) == 3  # untracked: refused
+        finally:
+            L.gdp_host_free(hptr)
+
+
+@pytest.mark.parametrize("defer", [False, True])
+def test_cpp_class_random_edit_sequences_with_write_tracking(oracle, tmp_path, defer):
     """Seeded random op sequences on GaussPyramid_hip (examples/state_hip): host edits (single
     floats, scaled rows, negated / zeroed levels, the input copy), calls (GenerateDoG, GaussFilter,
     GenerateDoG_mpi, GaussPyInit), mirror on / off with host_dirty / SyncDevice / SyncHost, and the
     write tracking switched off and on in between — the result must not depend on what the tracking
-    uploads: bit-identical to the oracle's replay of the same ops in every sequence."""
-    rng = np.random.default_rng(606)
+    uploads: bit-identical to the oracle's replay of the same ops in every sequence.  With `defer`,
+    the deferred download (DeferDownload) is switched on and off in between as well, starting on,
+    and whole-pyramid reads interleave: what GaussPy shows must not depend on when it is fetched."""
+    rng = np.random.default_rng(606 if not defer else 616)
     for case in range(16):
         n = int(rng.choice([64, 100, 32]))
         O = oracle.octaves(n)
@@ -532,12 +634,39 @@ def test_cpp_class_random_edit_sequences_with_write_tracking(oracle, tmp_path):
             elif k < 0.62:
                 ops.append(str(rng.choice([f"neg:{o}:{s_}", f"zero:{o}:{s_}"])))
             elif k < 0.70:
-                ops.append(str(rng.choice(["track:0", "track:1", "written"])))
+                ops.append(str(rng.choice(["track:0", "track:1", "written"] + (["defer:0", "defer:1", "read"] if defer else []))))
             elif k < 0.80:
                 ops.append(str(rng.choice(["mirror:0", "mirror:1", "dirty", "syncdev", "synchost"])))
             elif k < 0.87:
                 ops.append(f"data:{int(rng.integers(0, n))}:{int(rng.integers(0, n))}:{int(rng.integers(-500, 500))}")
             else:
                 ops.append(str(rng.choice(["init", "dog"])))
+        if defer:
+            ops.insert(0, "defer:1")
         ops += ["mirror:1", "dog"]  # end on a mirrored call so GaussPy holds the final state
-        _run(oracle, tmp_path, "hip", n, 2, f"lcg:{700 + case}", ops)
+        _run(oracle, tmp_path, "hip", n, 2, f"lcg:{(800 if defer else 700) + case}", ops)
+
+
+def test_cpp_class_deferred_download(oracle, tmp_path):
+    """DeferDownload(true): a mutating call leaves GaussPy's pages inaccessible (stale = the whole
+    mirror, nothing copied back) and the first access to a page fetches its neighbourhood; values
+    read, edited and dumped are bit-identical to the eager mirror's.  A write after a call is
+    recorded (one page uploaded by the next call); the mirror off in between fetches first (the
+    host keeps the deferred call's state); re-seated rows, SyncHost, GaussPyInit and the MPI entry
+    keep the same bits; DeferDownload(false) completes the mirror."""
+    page = os.sysconf("SC_PAGESIZE")
+    n, S = 64, 2
+    (w, st) = _run(oracle, tmp_path, "hip", n, S, "lcg:21", ["defer:1", "dog", "stale", "written", "dog", "stale",
+                                                            "set:0:0:3:7:-1e30", "written", "dog", "written", "read",
+                                                            "stale"], want_stale=True)
+    assert w == [0, page, 0], w
+    assert st[0] > 0 and st[1] == st[0] and st[2] == 0, st  # the read fetched every page
+    (w, st) = _run(oracle, tmp_path, "hip", 100, S, "lcg:22", ["defer:1", "dog", "mirror:0", "dog", "stale", "mirror:1",
+                                                              "neg:0:1", "dog", "filter:1", "mpi", "stale", "defer:0",
+                                                              "stale"], want_stale=True)
+    assert st[0] == 0 and st[1] > 0 and st[2] == -1, st
+    _run(oracle, tmp_path, "hip", n, S, "lcg:23", ["defer:1", "dog", "reseat:0:1:7", "scale:0:1:7:-2", "dog",
+                                                   "synchost", "dog", "init", "zero:0:2", "dog"])
+    _run(oracle, tmp_path, "hip", n, S, "lcg:24", ["defer:1", "init", "dog", "track:0", "neg:1:0", "dog", "track:1",
+                                                   "defer:1", "dog", "scale:1:1:3:0.5", "dog"])
+    _run(oracle, tmp_path, "a512xp", n, S, "lcg:25", ["defer:1", "dog", "set:0:1:2:2:-4", "filter:0", "dog"])

@@ -150,7 +150,34 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
             OK(gdp_host_track(t, raw.size() * 4));  // tracking back on (not armed)
             OK(gdp_upload_image_written(c, 0, t));  // not armed: the whole mirror, then armed
             OK(gdp_host_written_bytes(t, &wb));
-            gdp_host_free(tv);
+            // the deferred download: pages fetched on touch (a helper thread's copies), a write
+            // recorded, completion by gdp_host_fetch / a whole download / gdp_destroy's settle
+            OK(gdp_generate_dog(c, nullptr));
+            OK(gdp_host_defer(c, 0, t));
+            size_t st = 0, fb = 0;
+            uint64_t nf = 0;
+            OK(gdp_host_deferred_stats(t, &st, &fb, &nf));
+            EXPECT(st >= raw.size() * 4 && fb == 0 && nf == 0);
+            std::vector<float> dev(raw.size());
+            OK(gdp_download_image_raw(c, 0, dev.data()));
+            EXPECT(t[raw.size() / 2] == dev[raw.size() / 2] || (t[raw.size() / 2] != t[raw.size() / 2]));
+            t[1] = 4.0f;
+            dev[1] = 4.0f;
+            OK(gdp_host_written_bytes(t, &wb));
+            EXPECT(wb > 0);
+            OK(gdp_host_fetch(t));
+            OK(gdp_host_deferred_stats(t, &st, &fb, &nf));
+            EXPECT(st == 0 && nf > 0);
+            EXPECT(std::memcmp(t, dev.data(), raw.size() * 4) == 0);
+            OK(gdp_upload_image_written(c, 0, t));
+            OK(gdp_host_defer(c, 0, t));
+            OK(gdp_download_image_raw(c, 0, t));  // ends the deferral
+            OK(gdp_host_deferred_stats(t, &st, nullptr, nullptr));
+            EXPECT(st == 0);
+            OK(gdp_host_defer(c, 0, t));
+            EXPECT(gdp_host_deferred_stats(nullptr, &st, nullptr, nullptr) == GDP_ERR_ARG);
+            EXPECT(gdp_host_fetch(nullptr) == GDP_ERR_ARG);
+            gdp_host_free(tv);  // freed while deferred
         }
         EXPECT(gdp_generate_dog_mirrored(c, 1 << 20, raw.data()) == GDP_ERR_ARG);
         EXPECT(gdp_generate_dog_mirrored(c, 0, nullptr) == GDP_ERR_ARG);
