@@ -4,7 +4,8 @@
 // (MPI singleton, one rank).  Parity mode: mpi_hip [n] [lcg:SEED|ones] [dump.f32] [calls] [mixed]
 // — `calls` GenerateDoG_mpi calls on the same object (default 1); with "mixed" a single-process
 // GenerateDoG() runs between consecutive GenerateDoG_mpi calls; with "edit" the collector edits its
-// GaussPy between them (level (0, 1) zeroed, row 3 of level (0, 0) scaled by -2: two-way state).
+// GaussPy between them (level (0, 1) zeroed, row 3 of level (0, 0) scaled by -2: two-way state);
+// a 7th argument "defer" turns the deferred download on first (DeferDownload(true)).
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -37,6 +38,7 @@ int main(int argc, char* argv[]) {
         const int calls = argc > 4 ? std::atoi(argv[4]) : 1;
         const bool mixed = argc > 5 && std::string(argv[5]) == "mixed";
         const bool edit = argc > 5 && std::string(argv[5]) == "edit";
+        if (argc > 6 && std::string(argv[6]) == "defer") g.DeferDownload(true);
         for (int c = 0; c < calls; ++c) {
             if (c > 0 && mixed) g.GenerateDoG();
             if (c > 0 && edit && g.rank() == g.collector()) {
@@ -47,11 +49,18 @@ int main(int argc, char* argv[]) {
             g.GenerateDoG_mgpu(argc, argv);  // = GenerateDoG_mpi (the SURVEY's name for the RCCL form)
         }
         if (g.rank() == g.collector()) {  // rank 0, or S+3 under the reference's role map (>= S+4 ranks)
+            // rows through a local copy (a deferred page must be touched by the CPU, not write(2))
             FILE* f = std::fopen(argv[3], "wb");
+            if (!f) return 3;
+            float* row = new float[n];
             for (int o = 0, len = n; len; ++o, len /= 2)
                 for (int sc = 0; sc < 5; ++sc)
-                    for (int r = 0; r < len; ++r) std::fwrite(g.GaussPy[o][sc][r], sizeof(float), len, f);
-            std::fclose(f);
+                    for (int r = 0; r < len; ++r) {
+                        for (int k = 0; k < len; ++k) row[k] = g.GaussPy[o][sc][r][k];
+                        if (std::fwrite(row, sizeof(float), len, f) != (size_t)len) return 3;
+                    }
+            delete[] row;
+            if (std::fclose(f) != 0) return 3;
         }
         return 0;
     }

@@ -8,6 +8,7 @@
 //   zero:O:S  neg:O:S  scale:O:S:R:F  set:O:S:R:C:V   edit level (O, S) of GaussPy
 //   reseat:O:S:R                           point GaussPy[O][S][R] at a fresh copy of the row
 //   mirror:0|1  dirty  syncdev  synchost   gdp_mpitest_mirror_host, _host_dirty, _SyncDevice(), _SyncHost()
+//   defer:0|1  stale                       gdp_mpitest_defer_download; print `stale=<bytes>` to stderr
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -39,6 +40,8 @@ static int apply(const std::string& spec, int** p, int argc, char** argv) {
     else if (op == "dirty") gdp_mpitest_host_dirty = true;
     else if (op == "syncdev") gdp_mpitest_SyncDevice();
     else if (op == "synchost") gdp_mpitest_SyncHost();
+    else if (op == "defer") gdp_mpitest_defer_download = num(1) != 0;
+    else if (op == "stale") std::fprintf(stderr, "stale=%lld\n", gdp_mpitest_stale_bytes());
     else if (op == "zero" || op == "neg" || op == "scale" || op == "set" || op == "reseat") {
         const int o = num(1), s = num(2), len = n >> o;
         if (op == "zero" || op == "neg") {
@@ -89,11 +92,18 @@ int main(int argc, char* argv[]) {
         GenerateDoG_mpi_omp(argc, argv);
     }
     if (argc > 3) {
+        // rows through a local copy: a long fwrite may pass the row to write(2), which fails on a
+        // deferred page not fetched yet (the copy's reads fetch it)
         FILE* f = std::fopen(argv[3], "wb");
+        if (!f) return 3;
+        std::vector<float> row(n);
         for (int o = 0; o < layer; ++o)
             for (int sc = 0; sc < S + 3; ++sc)
-                for (int r = 0; r < (n >> o); ++r) std::fwrite(GaussPy[o][sc][r], sizeof(float), n >> o, f);
-        std::fclose(f);
+                for (int r = 0; r < (n >> o); ++r) {
+                    std::memcpy(row.data(), GaussPy[o][sc][r], sizeof(float) * (n >> o));
+                    if (std::fwrite(row.data(), sizeof(float), n >> o, f) != (size_t)(n >> o)) return 3;
+                }
+        if (std::fclose(f) != 0) return 3;
     }
     delete_mpi();
     return 0;

@@ -101,6 +101,18 @@ public:
     bool host_dirty = false;  // the caller edited GaussPy / data: upload before the next call
     void SyncHost() { sync_host_(); host_current_ = true; }
     void SyncDevice();        // upload GaussPy into this rank's whole-image state now
+    // Deferred download (opt-in, as GaussPyramid_hip::DeferDownload): where GaussPy would be
+    // refreshed after a call, its pages are left to be fetched from this rank's whole-image state
+    // when first touched.  Returns whether it is on (needs the write-tracked mirror).
+    bool DeferDownload(bool on) {
+        if (!on && defer_) check_(gdp_host_fetch(host_), "DeferDownload", full_);
+        defer_ = on && track_ && host_;
+        return defer_;
+    }
+    long long stale_bytes() const {  // bytes of GaussPy still to be fetched, -1 when not deferring
+        size_t b = 0;
+        return defer_ && gdp_host_deferred_stats(host_, &b, nullptr, nullptr) == GDP_OK ? (long long)b : -1;
+    }
 
 protected:
     int length;
@@ -147,8 +159,23 @@ protected:
     }
     bool track_ = false;  // host_ is write-tracked (gdp_host_alloc_tracked, GaussDePyramid-HIP.h)
     bool armed_ = false;  // ... and equals full_'s pyramid as of its arming
+    bool defer_ = false;  // DeferDownload
     void arm_() {
         armed_ = track_ && rows_in_mirror_() && gdp_host_arm(host_) == GDP_OK;
+    }
+    // after a call that changed full_ with mirror_host: GaussPy shows it — deferred, or copied now
+    void publish_() {
+        if (defer_ && rows_in_mirror_() && gdp_host_defer(full_, 0, host_) == GDP_OK) {
+            armed_ = true;
+            host_current_ = true;
+            return;
+        }
+        SyncHost();
+    }
+    // before a call that changes full_: a deferred GaussPy that the call will not defer again
+    // (`republished` false: mirror off, rows re-seated) is fetched while full_ still holds it
+    void keep_deferred_(bool republished) {
+        if (defer_ && !(republished && rows_in_mirror_())) check_(gdp_host_fetch(host_), "DeferDownload", full_);
     }
     // the error text is read only after the failing call returned (never as a sibling argument,
     // whose evaluation order relative to the call is unspecified)
@@ -258,28 +285,31 @@ inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GP
             check_(gdp_set_input_rows(band_, 0, (const int32_t* const*)(data + r0), nullptr), "GaussPyInit", band_);
     }
     host_dirty = false;
+    keep_deferred_(mirror_host);
     armed_ = false;  // every level is refilled on the device
     check_(gdp_init(full_, nullptr), "GaussPyInit", full_);
     is_initialized = true;
     fresh_ = true;
     band_live_ = false;
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
     else host_current_ = false;
 }
 
 inline void GaussPyramid_hip_mpi::GaussFilter(int theLayer) {  // :133-167
+    keep_deferred_(mirror_host);
     pull_host_();
     check_(gdp_gauss_octave(full_, theLayer, nullptr), "GaussFilter", full_);
     fresh_ = band_live_ = false;
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
     else host_current_ = false;
 }
 
 inline void GaussPyramid_hip_mpi::GenerateDoG() {  // :169-183 (single process, current contents)
+    keep_deferred_(mirror_host);
     pull_host_();
     check_(gdp_generate_dog(full_, nullptr), "GenerateDoG", full_);
     fresh_ = band_live_ = false;
-    if (mirror_host) SyncHost();
+    if (mirror_host) publish_();
     else host_current_ = false;
 }
 
@@ -307,6 +337,7 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
         ref_roles_ = reference_roles(roles, size_, S);
     }
     if (ref_roles_) {  // GaussDePyramid-MPI.h:265-335, role for role
+        keep_deferred_(rank_ > S + 3 || mirror_host);  // ranks <= S+3 change full_ below
         pull_host_();
         const int L = S + 3;
         if (rank_ < L) {  // worker: window this rank's scale of every octave (:271-284)
@@ -321,7 +352,7 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
         check_(gdp_sync(full_), "GenerateDoG_mpi", full_);
         fresh_ = band_live_ = false;
         if (rank_ <= L) {
-            if (mirror_host) SyncHost();
+            if (mirror_host) publish_();
             else host_current_ = false;
         }
         return;
@@ -339,6 +370,7 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
                    band_);
         }
     }
+    keep_deferred_(rank_ != 0 || mirror_host);  // the gather changes rank 0's full_ only
     pull_host_();
     // every rank takes the same (collective) path; only where its band starts from differs
     if (band_) {
@@ -354,7 +386,7 @@ inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :
                 comm_);
     fresh_ = false;
     band_live_ = true;
-    if (rank_ == 0 && mirror_host) SyncHost();
+    if (rank_ == 0 && mirror_host) publish_();
     else host_current_ = false;  // workers: the result rows live in the band context
 }
 

@@ -22,6 +22,8 @@
 // and edits reach the device only with `gdp_mpitest_host_dirty = true` (the next call uploads first)
 // or gdp_mpitest_SyncDevice().  Only in that mode may a GenerateDoG_* right after GaussPyInit use
 // the fused build (GaussPyInit + GenerateDoG in one pass, bit-identical on unedited contents).
+// `gdp_mpitest_defer_download = true` (opt-in) replaces the copy back by the deferred download
+// (pages fetched from the device when first touched).
 // Window centre: mpitest.cpp centres on the INTEGER octave length, `l = float(len - 1) / 2.0`
 // (:44, :123), not on GuassDePyramid.h's float-halved length (:107-115); the context uses the same
 // (GDP_CENTRE_INTLEN), so the result equals mpitest.cpp's collector for every n — the two centres
@@ -60,6 +62,11 @@ bool gdp_mpitest_host_dirty = false;  // mirror off: the caller edited GaussPy, 
 bool gdp_mpitest_track_writes = true;
 static bool gdp_mpitest_tracked = false;  // gdp_mpitest_host is gdp_host_alloc_tracked memory
 static bool gdp_mpitest_armed = false;    // ... protected since it last equalled the device copy
+// deferred download (opt-in; needs the tracked mirror): GaussPyInit / GenerateDoG_*
+// leave GaussPy's pages to be fetched from the device when first touched instead of copying the
+// pyramid back (gdp_host_defer).  Read at every call; a caller that hands GaussPy to system calls
+// reading it (write(2) of a row) calls gdp_mpitest_SyncHost() first.
+bool gdp_mpitest_defer_download = false;
 
 static inline void gdp_mpitest_check(int status, const char* what) {
     if (status != GDP_OK) {
@@ -92,6 +99,26 @@ static inline int gdp_mpitest_download() {
                                                 : gdp_download_pyramid_rows(gdp_mpitest_ctx, 0, GaussPy);
     if (rc == GDP_OK) gdp_mpitest_arm();
     return rc;
+}
+
+static inline bool gdp_mpitest_deferring() {
+    return gdp_mpitest_defer_download && gdp_mpitest_tracked && gdp_mpitest_rows_in_mirror();
+}
+
+// after a call: GaussPy shows the device pyramid — deferred, or copied now
+static inline int gdp_mpitest_publish() {
+    if (gdp_mpitest_deferring() && gdp_host_defer(gdp_mpitest_ctx, 0, gdp_mpitest_host) == GDP_OK) {
+        gdp_mpitest_armed = true;  // pages fetched and then written are recorded from here on
+        return GDP_OK;
+    }
+    return gdp_mpitest_download();
+}
+
+// bytes of GaussPy still to be fetched (-1: nothing deferred / not tracked)
+inline long long gdp_mpitest_stale_bytes() {
+    size_t b = 0;
+    return gdp_mpitest_tracked && gdp_host_deferred_stats(gdp_mpitest_host, &b, nullptr, nullptr) == GDP_OK ? (long long)b
+                                                                                                          : -1;
 }
 
 // GaussPy (the host pyramid, possibly edited) -> the device pyramid now
@@ -142,14 +169,14 @@ void GaussPyInit(int* data[MAX]) {
     gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
     gdp_mpitest_host_dirty = false;  // every level refilled: host edits are overwritten, as in :462-472
     gdp_mpitest_fresh = true;
-    gdp_mpitest_check(gdp_mpitest_download(), "GaussPyInit");
+    gdp_mpitest_check(gdp_mpitest_publish(), "GaussPyInit");
 }
 
 static inline void gdp_mpitest_generate() {
     auto begin = std::chrono::steady_clock::now();
     // the GLOBAL GaussPy is what the reference's workers multiply and its collector subtracts
     // (:128-133, :165): upload it first, then the in-place pass on exactly those contents
-    if (gdp_mpitest_mirror_host && gdp_mpitest_rows_in_mirror()) {
+    if (gdp_mpitest_mirror_host && gdp_mpitest_rows_in_mirror() && !gdp_mpitest_deferring()) {
         // upload (the written pages only, when armed) + in-place pass + download in one call,
         // pipelined over row chunks
         const bool clean = gdp_mpitest_armed;
@@ -160,12 +187,20 @@ static inline void gdp_mpitest_generate() {
         gdp_mpitest_arm();
         gdp_mpitest_host_dirty = false;
     } else {
-        gdp_mpitest_armed = false;  // the device changes below; the download re-arms
-        if (gdp_mpitest_mirror_host || gdp_mpitest_host_dirty) gdp_mpitest_SyncDevice();
+        const bool clean = gdp_mpitest_armed;
+        gdp_mpitest_armed = false;  // the device changes below; the download / deferral re-arms
+        if (gdp_mpitest_mirror_host || gdp_mpitest_host_dirty) {
+            if (clean && gdp_mpitest_rows_in_mirror())  // the written pages only (deferred mirrors)
+                gdp_mpitest_check(gdp_upload_image_written(gdp_mpitest_ctx, 0, gdp_mpitest_host), "GenerateDoG_mpi");
+            else
+                gdp_mpitest_SyncDevice();
+            gdp_mpitest_host_dirty = false;
+            gdp_mpitest_fresh = false;
+        }
         gdp_mpitest_check(gdp_mpitest_fresh ? gdp_build(gdp_mpitest_ctx, nullptr) : gdp_generate_dog(gdp_mpitest_ctx, nullptr),
                           "GenerateDoG_mpi");
         gdp_mpitest_check(gdp_sync(gdp_mpitest_ctx), "GenerateDoG_mpi");
-        gdp_mpitest_check(gdp_mpitest_download(), "GenerateDoG_mpi");
+        gdp_mpitest_check(gdp_mpitest_publish(), "GenerateDoG_mpi");
     }
     gdp_mpitest_fresh = false;
     auto end = std::chrono::steady_clock::now();

@@ -951,16 +951,20 @@ def test_cpp_mpi_variant_dropin_collector(oracle, golden, tmp_path):
     n, spec, S = 100, "lcg:3", 2
     img = oracle.image_from_spec(n, spec)
     O = oracle.octaves(n)
-    for calls, mode in [(2, "mpi"), (3, "mpi"), (2, "mixed"), (3, "mixed")]:
-        subprocess.run([exe, str(n), spec, str(out), str(calls), mode], check=True, timeout=180, capture_output=True)
+    for calls, mode, defer in [(2, "mpi", []), (3, "mpi", []), (2, "mixed", []), (3, "mixed", []),
+                               (3, "mixed", ["defer"])]:
+        subprocess.run([exe, str(n), spec, str(out), str(calls), mode, *defer], check=True, timeout=180,
+                       capture_output=True)
         want = oracle.init_pyramid(img, S)
         for c in range(calls):
             if c > 0 and mode == "mixed":
                 oracle.generate_dog(want, n, n, S, O)  # single-process GenerateDoG: serial centre
             oracle.generate_dog(want, n, n, S, O, centre="intlen")
         _assert_same(np.fromfile(out, dtype=np.float32), want, ("mpi re-entry", calls, mode))
-    for calls in (2, 3):  # the collector's GaussPy edited between calls is what the next call processes
-        subprocess.run([exe, str(n), spec, str(out), str(calls), "edit"], check=True, timeout=180, capture_output=True)
+    for calls, defer in ((2, []), (3, []), (3, ["defer"])):  # the collector's GaussPy edited between calls
+        # is what the next call processes (also with the deferred download, round 6)
+        subprocess.run([exe, str(n), spec, str(out), str(calls), "edit", *defer], check=True, timeout=180,
+                       capture_output=True)
         want = oracle.init_pyramid(img, S)
         lv = oracle.levels(want, n, n, S, O)
         for c in range(calls):

@@ -238,6 +238,19 @@ def test_cpp_mpitest_without_mirror_uploads_only_when_told(oracle, tmp_path):
                                                    "synchost", "mpi"])
 
 
+def test_cpp_mpitest_deferred_download(oracle, tmp_path):
+    """gdp_mpitest_defer_download: GaussPyInit / GenerateDoG_* leave the global GaussPy to be
+    fetched on first touch; edits, re-seated rows, the mirror off and the flag toggled in between
+    give the eager mirror's bits."""
+    n, S = 64, 2
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:36", ["defer:1", "init", "mpi"] + EDITS + ["omp", "neg:0:0", "mpi"])
+    _run_mpitest(oracle, tmp_path, n, S, "lcg:37", ["defer:1", "mpi", "mirror:0", "zero:0:1", "mpi", "dirty",
+                                                   "scale:0:0:5:3", "mpi", "mirror:1", "defer:0", "set:1:2:3:4:5",
+                                                   "omp", "defer:1", "reseat:0:1:3", "scale:0:1:3:-2", "mpi"])
+    _run_mpitest(oracle, tmp_path, 100, S, "lcg:38", ["defer:1", "init", "syncdev", "mpi", "synchost", "neg:1:1",
+                                                     "mpi"])
+
+
 def test_python_mirror_processes_host_edits(pkg, oracle):
     """The Python GaussPyramid: writes through GaussPy[o][s] (element, row, whole level) and into
     `data` are processed by the next call, like the reference's float**** and data copy."""
