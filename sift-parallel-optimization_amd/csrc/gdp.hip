@@ -2317,7 +2317,14 @@ int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
     // caller says so for every page — it does not: only for the image it names)
     if (t->stale && (t->src_ctx != c || t->src != src) && track_settle(*t) != GDP_OK)
         return c->status(GDP_ERR_HIP, "gdp_host_defer: completing the previous deferral failed");
-    if (!g_fetch_worker.exchange(true)) std::thread(track_fetch_worker).detach();
+    if (!g_fetch_worker.exchange(true)) {
+        try {
+            std::thread(track_fetch_worker).detach();
+        } catch (...) {  // no copy thread: a fault could never be served, so refuse to defer
+            g_fetch_worker.store(false);
+            return c->status(GDP_ERR_STATE, "gdp_host_defer: the fetch thread could not be started");
+        }
+    }
     state_lock();
     const uintptr_t base = t->base.load(std::memory_order_relaxed);
     int rc = GDP_OK;
