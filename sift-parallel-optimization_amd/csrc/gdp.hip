@@ -35,6 +35,7 @@
 #include <vector>
 
 #include <linux/futex.h>
+#include <pthread.h>
 #include <sched.h>
 #include <signal.h>
 #include <sys/mman.h>
@@ -2318,6 +2319,8 @@ int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
     if (t->stale && (t->src_ctx != c || t->src != src) && track_settle(*t) != GDP_OK)
         return c->status(GDP_ERR_HIP, "gdp_host_defer: completing the previous deferral failed");
     if (!g_fetch_worker.exchange(true)) {
+        static bool atfork = false;  // a fork()ed child has no copy thread (and no mirrors: DONTFORK)
+        if (!atfork) atfork = pthread_atfork(nullptr, nullptr, [] { g_fetch_worker.store(false); }) == 0;
         try {
             std::thread(track_fetch_worker).detach();
         } catch (...) {  // no copy thread: a fault could never be served, so refuse to defer
