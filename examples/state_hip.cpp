@@ -16,6 +16,8 @@
 //   defer:0|1  stale                            DeferDownload; print `stale=<bytes>` to stderr
 //   read                                        read every GaussPy float once (fetches a deferred
 //                                               mirror page by page; prints `read_ms=` to stderr)
+//   readmt:T  negmt:O:S:T                       the read / neg:O:S from T threads at once, rows
+//                                               interleaved (concurrent faults on the mirror)
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -23,6 +25,7 @@
 #include <cstring>
 #include <iostream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "GaussDePyramid-HIP-AVX512.h"
@@ -69,7 +72,25 @@ static int run(G& g, int n, int S, const char* path, int nops, char** ops, int a
         else if (op == "written") std::fprintf(stderr, "written=%lld\n", g.written_bytes());
         else if (op == "defer") std::fprintf(stderr, "deferring=%d\n", (int)g.DeferDownload(num(1) != 0));
         else if (op == "stale") std::fprintf(stderr, "stale=%lld\n", g.stale_bytes());
-        else if (op == "read") {
+        else if (op == "readmt" || op == "negmt") {
+            const int T = num(op == "readmt" ? 1 : 3);
+            std::vector<std::thread> th;
+            std::vector<double> sums(T, 0.0);
+            for (int t = 0; t < T; ++t)
+                th.emplace_back([&, t] {
+                    int len = n;
+                    for (int o = 0; o < gdp_octaves_for(n); ++o, len /= 2)
+                        for (int sc = 0; sc < S + 3; ++sc) {
+                            if (op == "negmt" && (o != num(1) || sc != num(2))) continue;
+                            for (int r = t; r < len; r += T)
+                                for (int c = 0; c < len; ++c) {
+                                    if (op == "negmt") g.GaussPy[o][sc][r][c] = -g.GaussPy[o][sc][r][c];
+                                    else sums[t] += g.GaussPy[o][sc][r][c];
+                                }
+                        }
+                });
+            for (auto& x : th) x.join();
+        } else if (op == "read") {
             auto t0 = std::chrono::high_resolution_clock::now();
             double sum = 0;
             int len = n;

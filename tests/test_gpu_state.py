@@ -90,14 +90,14 @@ class _Replay:
             self.host[:] = self.pyr
         elif f[0] == "data":
             self.img[int(f[1]), int(f[2])] = int(f[3])
-        elif f[0] in ("reseat", "track", "written", "defer", "stale", "read"):
+        elif f[0] in ("reseat", "track", "written", "defer", "stale", "read", "readmt"):
             pass  # same contents, another address / the upload or download strategy / a report
         else:
             lv = self._lv(self.host, int(f[1]), int(f[2]))
-            if f[0] == "zero":
-                lv[:] = 0.0
-            elif f[0] == "neg":
+            if f[0] in ("neg", "negmt"):
                 lv[:] = -lv
+            elif f[0] == "zero":
+                lv[:] = 0.0
             elif f[0] == "scale":
                 lv[int(f[3])] *= np.float32(float(f[4]))
             elif f[0] == "set":
@@ -683,3 +683,14 @@ def test_cpp_class_deferred_download(oracle, tmp_path):
     _run(oracle, tmp_path, "hip", n, S, "lcg:24", ["defer:1", "init", "dog", "track:0", "neg:1:0", "dog", "track:1",
                                                    "defer:1", "dog", "scale:1:1:3:0.5", "dog"])
     _run(oracle, tmp_path, "a512xp", n, S, "lcg:25", ["defer:1", "dog", "set:0:1:2:2:-4", "filter:0", "dog"])
+
+
+def test_cpp_class_deferred_download_concurrent_faults(oracle, tmp_path):
+    """Several host threads touching a deferred GaussPy at once (a SIFT detector reading DoG levels
+    in parallel): concurrent read faults on stale pages and write faults on fetched ones are served
+    one at a time by the handler (fetches on the helper thread) — the values read and the edits
+    written from 8 threads give the oracle's bits, with and without deferral."""
+    for n in (256, 100):
+        for defer in ([], ["defer:1"]):
+            _run(oracle, tmp_path, "hip", n, 2, "lcg:26", defer + ["dog", "readmt:8", "negmt:0:1:8", "dog", "negmt:1:3:5",
+                                                                   "readmt:3", "dog", "negmt:0:0:8", "mpi"])
