@@ -55,6 +55,7 @@ public:
 };
 
 inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
+    CallScope scope(this);
     pull_host_();  // GaussPy is two-way state (GaussDePyramid-HIP.h)
     check_(ctx_, fresh_ ? gdp_build_subset(ctx_, nullptr) : gdp_generate_dog_subset(ctx_, nullptr),
            "GenerateDoG_nomp_dynamic");
@@ -64,6 +65,7 @@ inline void GaussPyramid_a512omp_hip::GenerateDoG_nomp_dynamic() {
 }
 
 inline void GaussPyramid_a512omp_hip::GenerateDoG() {
+    CallScope scope(this);
     // per octave (:183-201): the DoG pass, then once more where the side is <= 2 — as two
     // launches, all octaves and then the tiny ones
     pull_host_();

@@ -128,7 +128,22 @@ protected:
     bool armed_;  // the device pyramid equals host_ as of its last arming and the pages written
                   // since are recorded: the next mutating call may upload only those
     bool defer_;  // DeferDownload: mutating calls end in gdp_host_defer instead of SyncHost
-    bool rows_in_mirror_() const {  // every GaussPy row still where the constructor put it
+    // rows_in_mirror_() is a walk over every row pointer (41k at 4096^2, tens of microseconds):
+    // each public call takes it once (CallScope) and its helpers reuse the answer — the caller
+    // cannot re-seat a row while one of its calls runs
+    mutable int rows_memo_ = -1;
+    mutable int call_depth_ = 0;
+    struct CallScope {
+        const GaussPyramid_hip* g;
+        explicit CallScope(const GaussPyramid_hip* g_) : g(g_) {
+            if (g->call_depth_++ == 0) g->rows_memo_ = g->rows_scan_() ? 1 : 0;
+        }
+        ~CallScope() {
+            if (--g->call_depth_ == 0) g->rows_memo_ = -1;
+        }
+    };
+    bool rows_in_mirror_() const { return rows_memo_ >= 0 ? rows_memo_ != 0 : rows_scan_(); }
+    bool rows_scan_() const {  // every GaussPy row still where the constructor put it
         if (!host_) return false;
         for (int o = 0; o < layer; ++o)
             for (int s = 0; s < S + 3; ++s) {
@@ -250,12 +265,14 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
 }
 
 inline void GaussPyramid_hip::SyncHost() {  // one DMA copy (pinned mirror) or one staged copy per 64 MiB
+    CallScope scope(this);
     check_(ctx_, rows_in_mirror_() ? gdp_download_image_raw(ctx_, 0, host_) : gdp_download_pyramid_rows(ctx_, 0, GaussPy),
            "SyncHost");
     arm_();
 }
 
 inline void GaussPyramid_hip::SyncDevice() {  // the inverse: the whole mirror, one H2D DMA copy or staged row gathers
+    CallScope scope(this);
     upload_();
     host_dirty = false;
     fresh_ = false;  // the contents are the caller's now, not necessarily GaussPyInit's
@@ -263,6 +280,7 @@ inline void GaussPyramid_hip::SyncDevice() {  // the inverse: the whole mirror, 
 }
 
 inline void GaussPyramid_hip::TrackWrites(bool on) {
+    CallScope scope(this);
     if (!on && track_) {
         check_(ctx_, gdp_host_untrack(host_), "TrackWrites");  // fetched if deferred; every page writable again
         track_ = armed_ = defer_ = false;
@@ -273,12 +291,14 @@ inline void GaussPyramid_hip::TrackWrites(bool on) {
 }
 
 inline bool GaussPyramid_hip::DeferDownload(bool on) {
+    CallScope scope(this);
     if (!on && defer_) check_(ctx_, gdp_host_fetch(host_), "DeferDownload");  // GaussPy complete again
     defer_ = on && track_ && host_;  // takes effect from the next mutating call
     return defer_;
 }
 
 inline void GaussPyramid_hip::GaussPyInit() {  // :60-87, from the CURRENT `data` (:80)
+    CallScope scope(this);
     keep_deferred_();
     armed_ = false;  // every level is refilled on the device
     if (mirror_host || host_dirty)
@@ -291,6 +311,7 @@ inline void GaussPyramid_hip::GaussPyInit() {  // :60-87, from the CURRENT `data
 }
 
 inline void GaussPyramid_hip::GaussFilter(int theLayer) {
+    CallScope scope(this);
     pull_host_();
     check_(ctx_, gdp_gauss_octave(ctx_, theLayer, nullptr), "GaussFilter");
     fresh_ = false;
@@ -298,6 +319,7 @@ inline void GaussPyramid_hip::GaussFilter(int theLayer) {
 }
 
 inline void GaussPyramid_hip::GenerateDoG() {
+    CallScope scope(this);
     if (piped_()) {
         // GaussPy mirrored in the pinned device-layout buffer: upload (only the pages written since
         // the last call when tracked), in-place pass and download in one call, pipelined over row
@@ -315,6 +337,7 @@ inline void GaussPyramid_hip::GenerateDoG() {
 }
 
 inline void GaussPyramid_hip::GenerateDoG_mpi(int, char**) {
+    CallScope scope(this);
     // switching centres selects the other device tap table (no drain, no re-upload after the
     // first call); both calls below are ordered on the context's stream
     const bool piped = piped_();  // see GenerateDoG

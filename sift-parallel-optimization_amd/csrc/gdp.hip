@@ -2097,6 +2097,7 @@ static void track_publish(TrackedMirror* t, void* host, size_t bytes, void* dma,
         t->written_cap = t->pages;
     }
     for (size_t p = 0; p < t->pages; ++p) t->written[p].store(0, std::memory_order_relaxed);
+    t->maybe_written.store(false, std::memory_order_relaxed);
     t->user = host;
     t->user_bytes = bytes;
     t->armed = false;
@@ -2189,6 +2190,7 @@ int gdp_host_untrack(void* host) try {
                        : GDP_ERR_STATE;
     t->armed = t->tracking = false;
     for (size_t p = 0; p < t->pages; ++p) t->written[p].store(0, std::memory_order_relaxed);
+    t->maybe_written.store(false, std::memory_order_relaxed);
     if (!t->dma) track_retire(t);  // an alias stays registered for its DMA view until gdp_host_free
     return rc;
 } GDP_ABI_CATCH(nullptr)
@@ -2214,7 +2216,7 @@ int gdp_host_written_bytes(const void* host, size_t* bytes) try {
     const uintptr_t b = t->base.load(std::memory_order_relaxed);
     const uintptr_t u0 = reinterpret_cast<uintptr_t>(t->user), u1 = u0 + t->user_bytes;
     size_t n = 0;
-    for (size_t p = 0; p < t->pages; ++p)
+    for (size_t p = t->maybe_written.load(std::memory_order_acquire) ? 0 : t->pages; p < t->pages; ++p)
         if (t->written[p].load(std::memory_order_relaxed) == kPageWritten) {
             const uintptr_t lo = std::max<uintptr_t>(u0, b + p * g_page_bytes);
             const uintptr_t hi = std::min<uintptr_t>(u1, b + (p + 1) * g_page_bytes);
@@ -2256,9 +2258,21 @@ int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
         std::lock_guard<std::mutex> lk(g_track_mu);
         t = track_for_image(c, host, &runs, &partial);
         // the written runs never cover a stale page; a whole upload needs every page current
-        if (!partial && track_settle_overlap(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(host) + (size_t)c->img_floats * 4) != GDP_OK)
+        if (!partial && track_settle_overlap(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(host) + (size_t)c->img_floats * 4) != GDP_OK) {
+            if (t) t->armed = false;
             return c->status(GDP_ERR_HIP, "gdp_upload_image_written: completing a deferred host mirror failed");
+        }
     }
+    // an error from here on leaves the collected runs un-uploaded: the next call uploads all
+    struct DisarmOnError {
+        TrackedMirror* t;
+        bool on = true;
+        ~DisarmOnError() {
+            if (!on || !t) return;
+            std::lock_guard<std::mutex> lk(g_track_mu);
+            t->armed = false;
+        }
+    } disarm{t};
     const char* src = static_cast<const char*>(track_dma_ptr(static_cast<const void*>(host)));
     GDP_HIP(c, hipSetDevice(c->device));
     char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
@@ -2269,6 +2283,7 @@ int gdp_upload_image_written(gdp_ctx* c, int b, const float* host) try {
         GDP_HIP(c, hipMemcpyAsync(dev, src, (size_t)c->img_floats * 4, hipMemcpyHostToDevice, c->stream));
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
+    disarm.on = false;
     std::lock_guard<std::mutex> lk(g_track_mu);
     if (t && track_rearm(*t, runs, !partial) != GDP_OK)
         return c->status(GDP_ERR_STATE, "gdp_upload_image_written: mprotect refused re-arming the mirror");
@@ -2285,8 +2300,10 @@ int gdp_generate_dog_mirrored_written(gdp_ctx* c, int b, float* host) try {
         std::lock_guard<std::mutex> lk(g_track_mu);
         t = track_for_image(c, host, &runs, &partial);
         // (as gdp_upload_image_written; the download at the end replaces every page)
-        if (!partial && track_settle_overlap(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(host) + (size_t)c->img_floats * 4) != GDP_OK)
+        if (!partial && track_settle_overlap(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(host) + (size_t)c->img_floats * 4) != GDP_OK) {
+            if (t) t->armed = false;
             return c->status(GDP_ERR_HIP, "gdp_generate_dog_mirrored_written: completing a deferred host mirror failed");
+        }
     }
     const int rc = generate_dog_mirrored(c, b, track_dma_ptr(host), partial ? &runs : nullptr);
     std::lock_guard<std::mutex> lk(g_track_mu);
@@ -2331,7 +2348,7 @@ int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
     state_lock();
     const uintptr_t base = t->base.load(std::memory_order_relaxed);
     int rc = GDP_OK;
-    for (size_t p = 0; p < t->pages;) {  // every page not stale yet: no access
+    for (size_t p = t->stale == t->pages ? t->pages : 0; p < t->pages;) {  // every page not stale yet: no access
         if (t->written[p].load(std::memory_order_relaxed) == kPageStale) {
             ++p;
             continue;
@@ -2354,6 +2371,7 @@ int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
     t->ra_next = t->ra_len = 0;
     t->fetched_bytes = 0;
     t->fetches = 0;
+    if (rc == GDP_OK) t->maybe_written.store(false, std::memory_order_relaxed);  // every page stale
     t->armed = rc == GDP_OK;  // no written page is pending: a record exists (nothing written yet)
     state_unlock();
     if (rc != GDP_OK) {
