@@ -99,7 +99,11 @@ public:
     }
     bool mirror_host = true;  // two-way GaussPy (see the header comment)
     bool host_dirty = false;  // the caller edited GaussPy / data: upload before the next call
-    void SyncHost() { sync_host_(); host_current_ = true; }
+    void SyncHost() {
+        CallScope scope(this);
+        sync_host_();
+        host_current_ = true;
+    }
     void SyncDevice();        // upload GaussPy into this rank's whole-image state now
     // Deferred download (opt-in, as GaussPyramid_hip::DeferDownload): where GaussPy would be
     // refreshed after a call, its pages are left to be fetched from this rank's whole-image state
@@ -130,7 +134,20 @@ protected:
     bool host_current_ = true;  // GaussPy mirrors full_ (false on workers after GenerateDoG_mpi)
     bool ref_roles_ = false;    // the reference's role map is in use (>= S+4 ranks)
     bool band_tried_ = false;   // the band context was planned (band split only)
-    bool rows_in_mirror_() const {
+    // the row walk once per public call (as GaussPyramid_hip's CallScope)
+    mutable int rows_memo_ = -1;
+    struct CallScope {
+        const GaussPyramid_hip_mpi* g;
+        bool outer;
+        explicit CallScope(const GaussPyramid_hip_mpi* g_) : g(g_), outer(g_->rows_memo_ < 0) {
+            if (outer) g->rows_memo_ = g->rows_scan_() ? 1 : 0;
+        }
+        ~CallScope() {
+            if (outer) g->rows_memo_ = -1;
+        }
+    };
+    bool rows_in_mirror_() const { return rows_memo_ >= 0 ? rows_memo_ != 0 : rows_scan_(); }
+    bool rows_scan_() const {
         if (!host_) return false;
         for (int o = 0; o < layer; ++o)
             for (int s = 0; s < S + 3; ++s) {
@@ -266,6 +283,7 @@ inline void GaussPyramid_hip_mpi::ensure_full_() {  // the whole-image context o
 }
 
 inline void GaussPyramid_hip_mpi::SyncDevice() {
+    CallScope scope(this);
     check_(rows_in_mirror_() ? gdp_upload_image_raw(full_, 0, host_)
                              : gdp_upload_pyramid_rows(full_, 0, (const float* const* const* const*)GaussPy),
            "SyncDevice", full_);
@@ -276,6 +294,7 @@ inline void GaussPyramid_hip_mpi::SyncDevice() {
 }
 
 inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GPU), from the CURRENT `data`
+    CallScope scope(this);
     const bool constructing = !is_initialized;  // the constructor just uploaded `data`
     ensure_full_();
     if (!constructing && (mirror_host || host_dirty)) {
@@ -296,6 +315,7 @@ inline void GaussPyramid_hip_mpi::GaussPyInit() {  // :87-114 (on this rank's GP
 }
 
 inline void GaussPyramid_hip_mpi::GaussFilter(int theLayer) {  // :133-167
+    CallScope scope(this);
     keep_deferred_(mirror_host);
     pull_host_();
     check_(gdp_gauss_octave(full_, theLayer, nullptr), "GaussFilter", full_);
@@ -305,6 +325,7 @@ inline void GaussPyramid_hip_mpi::GaussFilter(int theLayer) {  // :133-167
 }
 
 inline void GaussPyramid_hip_mpi::GenerateDoG() {  // :169-183 (single process, current contents)
+    CallScope scope(this);
     keep_deferred_(mirror_host);
     pull_host_();
     check_(gdp_generate_dog(full_, nullptr), "GenerateDoG", full_);
@@ -314,6 +335,7 @@ inline void GaussPyramid_hip_mpi::GenerateDoG() {  // :169-183 (single process, 
 }
 
 inline void GaussPyramid_hip_mpi::GenerateDoG_mpi(int argc, char** argv) {  // :265-335
+    CallScope scope(this);
     int inited = 0;
     MPI_Initialized(&inited);
     if (!inited) {

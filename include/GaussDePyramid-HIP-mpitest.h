@@ -77,7 +77,21 @@ static inline void gdp_mpitest_check(int status, const char* what) {
 
 // every GaussPy row still where GaussPyInit put it (a caller may re-seat one: the reference's rows
 // are separate new[] arrays, :451-453)
+static int gdp_mpitest_rows_memo = -1;  // the walk below, taken once per public call (gdp_mpitest_scope)
+static inline bool gdp_mpitest_rows_scan();
 static inline bool gdp_mpitest_rows_in_mirror() {
+    return gdp_mpitest_rows_memo >= 0 ? gdp_mpitest_rows_memo != 0 : gdp_mpitest_rows_scan();
+}
+struct gdp_mpitest_scope {  // the caller cannot re-seat a row while one of these functions runs
+    bool outer;
+    gdp_mpitest_scope() : outer(gdp_mpitest_rows_memo < 0) {
+        if (outer) gdp_mpitest_rows_memo = gdp_mpitest_rows_scan() ? 1 : 0;
+    }
+    ~gdp_mpitest_scope() {
+        if (outer) gdp_mpitest_rows_memo = -1;
+    }
+};
+static inline bool gdp_mpitest_rows_scan() {
     if (!gdp_mpitest_host) return false;
     for (int o = 0; o < layer; ++o)
         for (int s = 0; s < S + 3; ++s) {
@@ -123,6 +137,7 @@ inline long long gdp_mpitest_stale_bytes() {
 
 // GaussPy (the host pyramid, possibly edited) -> the device pyramid now
 inline void gdp_mpitest_SyncDevice() {
+    gdp_mpitest_scope scope;
     if (!is_initialized) return;
     gdp_mpitest_check(gdp_mpitest_rows_in_mirror()
                           ? gdp_upload_image_raw(gdp_mpitest_ctx, 0, gdp_mpitest_host)
@@ -135,6 +150,7 @@ inline void gdp_mpitest_SyncDevice() {
 
 // the device pyramid -> GaussPy now
 inline void gdp_mpitest_SyncHost() {
+    gdp_mpitest_scope scope;
     if (is_initialized) gdp_mpitest_check(gdp_mpitest_download(), "SyncHost");
 }
 
@@ -164,6 +180,7 @@ void GaussPyInit(int* data[MAX]) {
         }
     }
     is_initialized = true;
+    gdp_mpitest_scope scope;
     gdp_mpitest_armed = false;  // every level is refilled on the device
     gdp_mpitest_check(gdp_set_input_rows(gdp_mpitest_ctx, 0, (const int32_t* const*)data, nullptr), "GaussPyInit");
     gdp_mpitest_check(gdp_init(gdp_mpitest_ctx, nullptr), "GaussPyInit");
@@ -173,6 +190,7 @@ void GaussPyInit(int* data[MAX]) {
 }
 
 static inline void gdp_mpitest_generate() {
+    gdp_mpitest_scope scope;
     auto begin = std::chrono::steady_clock::now();
     // the GLOBAL GaussPy is what the reference's workers multiply and its collector subtracts
     // (:128-133, :165): upload it first, then the in-place pass on exactly those contents
