@@ -296,6 +296,12 @@ def dropin_call_cost(n=4096, calls=5):
                            text=True, timeout=120)
         m = re.search(r"([0-9.]+) ms per GenerateDoG", r.stderr)
         out[key] = float(m.group(1)) if (r.returncode == 0 and m) else None
+    # main.cpp's own size (n = 512, main.cpp:19): the default mirror and the deferred one
+    for key, ops in (("n512_mirror_host_ms", []), ("n512_mirror_deferred_ms", ["defer:1"])):
+        r = subprocess.run([exe, "hip", "512", "2", "ones", "-", *ops, "dog", f"time:{20 * calls}"], capture_output=True,
+                           text=True, timeout=120)
+        m = re.search(r"([0-9.]+) ms per GenerateDoG", r.stderr)
+        out[key] = float(m.group(1)) if (r.returncode == 0 and m) else None
     # reading every GaussPy float once after a call: eager mirror (already on the host) against the
     # deferred one (each page fetched on first touch) — the difference is what deferral moves to the
     # first read

@@ -257,6 +257,8 @@ inline GaussPyramid_hip_mpi::GaussPyramid_hip_mpi(int** img, int len, int S_) : 
         }
     }
     GaussPyInit();
+    if (const char* e = std::getenv("GDP_DEFER_DOWNLOAD"))  // as GaussPyramid_hip
+        if (e[0] == '1') DeferDownload(true);
 }
 
 // The rank this process will have, also before MPI_Init (main.cpp constructs the pyramid before

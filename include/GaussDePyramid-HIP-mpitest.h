@@ -66,7 +66,10 @@ static bool gdp_mpitest_armed = false;    // ... protected since it last equalle
 // leave GaussPy's pages to be fetched from the device when first touched instead of copying the
 // pyramid back (gdp_host_defer).  Read at every call; a caller that hands GaussPy to system calls
 // reading it (write(2) of a row) calls gdp_mpitest_SyncHost() first.
-bool gdp_mpitest_defer_download = false;
+bool gdp_mpitest_defer_download = [] {  // GDP_DEFER_DOWNLOAD=1 in the environment: on from the start
+    const char* e = std::getenv("GDP_DEFER_DOWNLOAD");
+    return e && e[0] == '1';
+}();
 
 static inline void gdp_mpitest_check(int status, const char* what) {
     if (status != GDP_OK) {

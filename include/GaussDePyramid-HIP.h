@@ -37,7 +37,7 @@
 //    Writes that do not fault on the CPU (read(2) into GaussPy — EFAULT on a protected page —, or
 //    DMA into it) are not seen: call TrackWrites(false) first, and every call uploads the whole
 //    mirror as before (also the fallback when page protection is unavailable).
-//    DeferDownload(true) (opt-in): the copy back is deferred too — after a mutating call GaussPy's
+//    DeferDownload(true) (opt-in; or GDP_DEFER_DOWNLOAD=1 in the environment): the copy back is deferred too — after a mutating call GaussPy's
 //    pages are inaccessible and the first access to one fetches its neighbourhood from the device
 //    (gdp_host_defer); main.cpp's loop then moves nothing over PCIe.  Reads see the same values.
 //  - mirror_host = false: the device pyramid is the state; GaussPy is refreshed only by
@@ -262,6 +262,10 @@ inline GaussPyramid_hip::GaussPyramid_hip(int** img, int len, int S_, int device
     initialized = true;
     fresh_ = true;
     if (mirror_host) SyncHost();
+    // GDP_DEFER_DOWNLOAD=1 in the environment turns the deferred download on for an unmodified
+    // caller (main.cpp after the two-line switch)
+    if (const char* e = std::getenv("GDP_DEFER_DOWNLOAD"))
+        if (e[0] == '1') DeferDownload(true);
 }
 
 inline void GaussPyramid_hip::SyncHost() {  // one DMA copy (pinned mirror) or one staged copy per 64 MiB

@@ -269,8 +269,8 @@ int gdp_generate_dog_mirrored(gdp_ctx* ctx, int b, float* host);
  * A mirror that the caller usually does not write (main.cpp's loop never writes GaussPy) need not
  * be uploaded before every call.  gdp_host_alloc_tracked: `bytes` of host memory for such a mirror
  * — one shared-memory object mapped twice, a view registered with HIP that libgdp's copies use
- * (gdp_upload_image_raw / gdp_download_image_raw / gdp_generate_dog_mirrored* given the returned
- * address DMA through it at the pinned rate) and the returned CPU view, which is the one ever
+ * (gdp_upload_image_raw / gdp_download_image_raw / gdp_generate_dog_mirrored* and the single-buffer
+ * level / pyramid copies given an address inside it DMA through it at the pinned rate) and the returned CPU view, which is the one ever
  * write-protected (protecting memory the GPU driver registered — hipHostMalloc / hipHostRegister —
  * invalidates the registration and stalls the process's GPU queues, so gdp_host_track refuses such
  * memory).  Freed by gdp_host_free.  GDP_ERR_STATE / _HIP / _NOMEM: not available (use

@@ -1551,7 +1551,7 @@ int gdp_download_level(gdp_ctx* c, int b, int o, int s, float* host) try {
     GDP_HIP(c, hipSetDevice(c->device));
     GDP_SETTLE(c, "gdp_download_level", [&](auto&& f) { f(host, (size_t)c->geom.oct[o].rows * c->geom.oct[o].cols * 4); });
     const OctGeom& og = c->geom.oct[o];
-    GDP_HIP(c, hipMemcpyAsync(host, gdp_device_level(c, b, o, s), (size_t)og.rows * og.cols * 4, hipMemcpyDeviceToHost,
+    GDP_HIP(c, hipMemcpyAsync(track_dma_ptr(host), gdp_device_level(c, b, o, s), (size_t)og.rows * og.cols * 4, hipMemcpyDeviceToHost,
                               c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1703,7 +1703,7 @@ int gdp_download_level_range(gdp_ctx* c, int b, int o, int s, int first_row, int
     GDP_HIP(c, hipSetDevice(c->device));
     GDP_SETTLE(c, "gdp_download_level_range", [&](auto&& f) { f(host, (size_t)nrows * c->geom.oct[o].cols * 4); });
     const OctGeom& og = c->geom.oct[o];
-    GDP_HIP(c, hipMemcpyAsync(host, gdp_device_level(c, b, o, s) + (size_t)first_row * og.cols,
+    GDP_HIP(c, hipMemcpyAsync(track_dma_ptr(host), gdp_device_level(c, b, o, s) + (size_t)first_row * og.cols,
                               (size_t)nrows * og.cols * 4, hipMemcpyDeviceToHost, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1718,7 +1718,7 @@ int gdp_download_pyramid(gdp_ctx* c, int b, float* host) try {
         const OctGeom& og = c->geom.oct[o];
         const size_t n = (size_t)og.rows * og.cols;
         for (int s = 0; s < c->geom.L; ++s, off += n)
-            if (n) GDP_HIP(c, hipMemcpyAsync(host + off, gdp_device_level(c, b, o, s), n * 4, hipMemcpyDeviceToHost, c->stream));
+            if (n) GDP_HIP(c, hipMemcpyAsync(track_dma_ptr(host + off), gdp_device_level(c, b, o, s), n * 4, hipMemcpyDeviceToHost, c->stream));
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1734,7 +1734,7 @@ int gdp_upload_pyramid(gdp_ctx* c, int b, const float* host) try {
         const size_t n = (size_t)og.rows * og.cols;
         for (int s = 0; s < c->geom.L; ++s, off += n)
             if (n)
-                GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), host + off, n * 4,
+                GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), track_dma_ptr(host + off), n * 4,
                                           hipMemcpyHostToDevice, c->stream));
     }
     GDP_HIP(c, hipStreamSynchronize(c->stream));
@@ -1815,7 +1815,7 @@ int gdp_upload_level(gdp_ctx* c, int b, int o, int s, const float* host) try {
     if ((size_t)og.rows * og.cols == 0) return GDP_OK;
     GDP_HIP(c, hipSetDevice(c->device));
     GDP_SETTLE(c, "gdp_upload_level", [&](auto&& f) { f(host, (size_t)og.rows * og.cols * 4); });
-    GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), host, (size_t)og.rows * og.cols * 4,
+    GDP_HIP(c, hipMemcpyAsync(const_cast<float*>(gdp_device_level(c, b, o, s)), track_dma_ptr(host), (size_t)og.rows * og.cols * 4,
                               hipMemcpyHostToDevice, c->stream));
     GDP_HIP(c, hipStreamSynchronize(c->stream));
     return GDP_OK;
@@ -1979,9 +1979,46 @@ int gdp_download_image_raw(gdp_ctx* c, int b, float* host) try {
 // (octave, row, column) across the S+3 levels, so any row split is exact.
 // `runs` (write-tracked mirrors): instead of every chunk, upload only these byte ranges of the
 // image (the pages written since the mirror was armed), all before the first chunk's pass.
+constexpr size_t kMirrorSerialBytes = 32u << 20;  // generate_dog_mirrored: unpipelined up to this image size
 static int generate_dog_mirrored(gdp_ctx* c, int b, float* host, const std::vector<std::pair<size_t, size_t>>* runs) {
     const Geom& g = c->geom;
     GDP_HIP(c, hipSetDevice(c->device));
+    auto pass = [&](int o, unsigned k0, unsigned k1, hipStream_t st) {  // octave o's groups [k0, k1) in place
+        auto kern = c->nontemporal ? k_levels_range<0, 3, true> : k_levels_range<0, 3, false>;
+        if (g.L == 5) kern = c->nontemporal ? k_levels_range<5, 3, true> : k_levels_range<5, 3, false>;
+        hipLaunchKernelGGL(kern, dim3((k1 - k0 + 255) / 256), dim3(256), 0, st, c->d_geom, c->d_out, c->d_taps,
+                           (unsigned)b, o, k0, k1);
+        return hipGetLastError();
+    };
+    // Small images (main.cpp's 512^2: 7 MB each way): the row-chunk pipeline's ~20 chunks of per-level
+    // copies and events cost more than the copies themselves, so one contiguous copy each way around
+    // one pass per octave, all on the context's stream.  Same bits (the op is pointwise).
+    const size_t img_bytes = (size_t)c->img_floats * 4;
+    if (img_bytes <= kMirrorSerialBytes) {
+        struct DrainOnError {  // (as below: no return while a copy of `host` is in flight)
+            gdp_ctx* c;
+            bool armed = true;
+            ~DrainOnError() {
+                if (armed) (void)hipStreamSynchronize(c->stream);
+            }
+        } drain{c};
+        char* dev = reinterpret_cast<char*>(c->d_out + (size_t)b * g.pyr_stride);
+        if (runs) {
+            for (const auto& r : *runs)
+                GDP_HIP(c, hipMemcpyAsync(dev + r.first, reinterpret_cast<const char*>(host) + r.first, r.second - r.first,
+                                          hipMemcpyHostToDevice, c->stream));
+        } else {
+            GDP_HIP(c, hipMemcpyAsync(dev, host, img_bytes, hipMemcpyHostToDevice, c->stream));
+        }
+        for (int o = 0; o < g.O; ++o) {
+            const unsigned k1 = (unsigned)g.oct[o].rows * (unsigned)g.oct[o].gpr;
+            if (k1) GDP_HIP(c, pass(o, 0u, k1, c->stream));
+        }
+        GDP_HIP(c, hipMemcpyAsync(host, dev, img_bytes, hipMemcpyDeviceToHost, c->stream));
+        GDP_HIP(c, hipStreamSynchronize(c->stream));
+        drain.armed = false;
+        return GDP_OK;
+    }
     if (!c->st_up) GDP_HIP(c, hipStreamCreateWithFlags(&c->st_up, hipStreamNonBlocking));
     if (!c->st_down) GDP_HIP(c, hipStreamCreateWithFlags(&c->st_down, hipStreamNonBlocking));
     // chunks of about 1/16 of the image's bytes: octave 0 in ~12 row ranges, each smaller octave in
@@ -2040,11 +2077,7 @@ static int generate_dog_mirrored(gdp_ctx* c, int b, float* host, const std::vect
         GDP_HIP(c, hipEventRecord(ev[2 * j], c->st_up));
         GDP_HIP(c, hipStreamWaitEvent(c->stream, ev[2 * j], 0));
         const unsigned k0 = (unsigned)ch.r0 * (unsigned)og.gpr, k1 = (unsigned)ch.r1 * (unsigned)og.gpr;
-        auto kern = c->nontemporal ? k_levels_range<0, 3, true> : k_levels_range<0, 3, false>;
-        if (g.L == 5) kern = c->nontemporal ? k_levels_range<5, 3, true> : k_levels_range<5, 3, false>;
-        hipLaunchKernelGGL(kern, dim3((k1 - k0 + 255) / 256), dim3(256), 0, c->stream, c->d_geom, c->d_out, c->d_taps,
-                           (unsigned)b, ch.o, k0, k1);
-        GDP_HIP(c, hipGetLastError());
+        GDP_HIP(c, pass(ch.o, k0, k1, c->stream));
         GDP_HIP(c, hipEventRecord(ev[2 * j + 1], c->stream));
         GDP_HIP(c, hipStreamWaitEvent(c->st_down, ev[2 * j + 1], 0));
         for (int s = 0; s < g.L; ++s)

@@ -984,9 +984,18 @@ def test_reference_drivers_run_on_the_dropin(tmp_path):
     if not os.path.exists(main):
         pytest.skip("oracle/_ref/dropin_* not built (needs the reference sources at build time)")
     r = subprocess.run([main], check=True, timeout=180, capture_output=True, text=True)
-    assert float(r.stdout.split()[-1]) > 0  # main.cpp:74 mean ms per GenerateDoG_mpi call
+    eager = float(r.stdout.split()[-1])
+    assert eager > 0  # main.cpp:74 mean ms per GenerateDoG_mpi call
+    # the same unmodified driver with the deferred download switched on from the environment: its
+    # loop never reads GaussPy, so no call copies the pyramid back (n = 512: 7 MB per call)
+    env = dict(os.environ, GDP_DEFER_DOWNLOAD="1")
+    r = subprocess.run([main], check=True, timeout=180, capture_output=True, text=True, env=env)
+    deferred = float(r.stdout.split()[-1])
+    assert 0 < deferred < eager, (deferred, eager)
     r = subprocess.run([mpitest], check=True, timeout=180, capture_output=True, text=True)
     assert float(r.stdout.split()[-1]) >= 0  # elapsed seconds (mpitest.cpp:95-96)
+    r = subprocess.run([mpitest], check=True, timeout=180, capture_output=True, text=True, env=env)
+    assert float(r.stdout.split()[-1]) >= 0
     if os.path.exists(mpi):
         for cmd in ([mpi], ["/opt/conda/bin/mpiexec", "-n", "1", mpi]):
             if cmd[0].startswith("/opt") and not os.path.exists(cmd[0]):

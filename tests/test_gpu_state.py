@@ -513,6 +513,19 @@ def test_tracked_mirror_uploads_only_written_pages(pkg, oracle):
             assert L.gdp_upload_image_written(m._ctx, 0, hptr) == 0
             assert L.gdp_download_image_raw(m._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
             _assert_same(got, ref, "gdp_upload_image_written")
+            # single-level copies given an address inside the mirror DMA through its registered view:
+            # level (0, 0) of context a (which never saw the 2.5 row) into the mirror, then the mirror's
+            # level up into m
+            lo, (rows, cols) = a.level_offset(0, 0, 0), a.level_dims(0)[:2]
+            want = np.empty(rows * cols, np.float32)
+            assert L.gdp_download_level(a._ctx, 0, 0, 0, want.ctypes.data_as(ctypes.c_void_p)) == 0
+            assert L.gdp_download_level(a._ctx, 0, 0, 0, ctypes.c_void_p(hptr.value + 4 * lo)) == 0
+            _assert_same(host[lo:lo + rows * cols], want, "gdp_download_level into the tracked mirror")
+            assert L.gdp_upload_level(m._ctx, 0, 0, 0, ctypes.c_void_p(hptr.value + 4 * lo)) == 0
+            lv = np.empty(rows * cols, np.float32)
+            assert L.gdp_download_level(m._ctx, 0, 0, 0, lv.ctypes.data_as(ctypes.c_void_p)) == 0
+            _assert_same(lv, want, "gdp_upload_level from the tracked mirror")
+            ref[lo:lo + rows * cols] = want
             assert L.gdp_host_untrack(hptr) == 0  # writable, not recorded; the DMA view stays
             host[5] = np.float32(1.0)
             assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 3
