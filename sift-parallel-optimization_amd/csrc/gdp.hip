@@ -2366,7 +2366,7 @@ int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
     const char* src = reinterpret_cast<const char*>(c->d_out + (size_t)b * c->geom.pyr_stride);
     // stale pages of ANOTHER source are fetched first (they are older than this image only if the
     // caller says so for every page — it does not: only for the image it names)
-    if (t->stale && (t->src_ctx != c || t->src != src) && track_settle(*t) != GDP_OK)
+    if ((t->stale || t->trips) && (t->src_ctx != c || t->src != src) && track_settle(*t) != GDP_OK)
         return c->status(GDP_ERR_HIP, "gdp_host_defer: completing the previous deferral failed");
     if (!g_fetch_worker.exchange(true)) {
         static bool atfork = false;  // a fork()ed child has no copy thread (and no mirrors: DONTFORK)
@@ -2378,16 +2378,27 @@ int gdp_host_defer(gdp_ctx* c, int b, void* host) try {
             return c->status(GDP_ERR_STATE, "gdp_host_defer: the fetch thread could not be started");
         }
     }
-    state_lock();
+    state_lock_quiesced();  // no copy of an older deferral still landing
     const uintptr_t base = t->base.load(std::memory_order_relaxed);
     int rc = GDP_OK;
-    for (size_t p = t->stale == t->pages ? t->pages : 0; p < t->pages;) {  // every page not stale yet: no access
-        if (t->written[p].load(std::memory_order_relaxed) == kPageStale) {
+    // every page not stale yet: no access (tripwires are inaccessible already)
+    auto open = [&](size_t p) {
+        const unsigned char st = t->written[p].load(std::memory_order_relaxed);
+        return st == kPageClean || st == kPageWritten;
+    };
+    for (size_t p = t->stale == t->pages ? t->pages : 0; p < t->pages;) {
+        const unsigned char st = t->written[p].load(std::memory_order_relaxed);
+        if (st == kPageTrip) {
+            t->written[p].store(kPageStale, std::memory_order_relaxed);
+            --t->trips;
+            ++t->stale;
+        }
+        if (!open(p)) {
             ++p;
             continue;
         }
         size_t q = p + 1;
-        while (q < t->pages && t->written[q].load(std::memory_order_relaxed) != kPageStale) ++q;
+        while (q < t->pages && open(q)) ++q;
         if (mprotect(reinterpret_cast<void*>(base + p * g_page_bytes), (q - p) * g_page_bytes, PROT_NONE) != 0) {
             rc = GDP_ERR_STATE;
             break;

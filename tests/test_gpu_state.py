@@ -592,8 +592,9 @@ def test_deferred_mirror_fetches_on_first_touch(pkg, oracle):
             assert L.gdp_host_written_bytes(hptr, ctypes.byref(written)) == 0 and written.value == page
             _assert_same(host, ref, "whole deferred mirror after the touches")  # fetches the rest
             st, fb, nf = stats()
-            # (a sequential copy stops at each block the random reads fetched: at most two more each)
-            assert st == 0 and nf <= 2 * 40 + 40, (st, fb, nf)
+            # (a sequential copy stops at each block the random reads fetched and restarts with a
+            # block and its read-ahead after it: a few more copies each)
+            assert st == 0 and nf <= 4 * 40 + 40, (st, fb, nf)
             # the written page goes up with the next written-page upload; a pass and a new deferral
             assert L.gdp_upload_image_written(a._ctx, 0, hptr) == 0
             assert L.gdp_download_image_raw(a._ctx, 0, got.ctypes.data_as(ctypes.c_void_p)) == 0
