@@ -303,14 +303,16 @@ int gdp_generate_dog_mirrored_written(gdp_ctx* ctx, int b, float* host);
  * gdp_host_alloc_tracked buffer `host` (at most gdp_image_floats floats), instead of downloading
  * it: every page of the CPU view becomes inaccessible, and the first CPU access to one (read or
  * write) faults, has a block of pages around it copied from the device — 64 pages, doubling to 8192
- * while the faults walk forward — on the context's stream by a libgdp helper thread, and arms them
+ * while the faults walk forward, then the next block ahead of the reader too (its first page stays
+ * inaccessible until touched, which queues the one after) — on the context's stream by a libgdp
+ * helper thread, and arms them
  * (a write then faults once more and is recorded, as above).  Not blocking: the fetches are ordered
  * after the work queued on the context's stream.  Host writes not uploaded yet are discarded (the
  * device copy is declared the newer one).  gdp_host_fetch completes a deferred buffer now (every
  * inaccessible page fetched; gdp_download_image_raw(b, host) of the whole image ends the deferral
  * by overwriting it).  Every libgdp entry taking caller host memory completes deferred buffers
  * first, and gdp_destroy completes those deferred to its context; gdp_host_untrack / gdp_host_arm
- * of a deferred buffer complete it first.  gdp_host_deferred_stats: inaccessible bytes (whole
+ * of a deferred buffer complete it first.  gdp_host_deferred_stats: bytes not fetched yet (whole
  * pages) and the bytes / copies fetched since the last gdp_host_defer (any argument may be NULL).
  * Limits on top of write tracking's: a system call READING a deferred page (write(2), send(2) from
  * it) fails with EFAULT, and a fault while the faulting thread holds a HIP runtime lock (the
