@@ -632,6 +632,87 @@ def test_deferred_mirror_fetches_on_first_touch(pkg, oracle):
             L.gdp_host_free(hptr)
 
 
+def test_deferred_mirror_random_sequences(pkg, oracle):
+    """Seeded random sequences on the C ABI of the tracked mirror (round 6): CPU reads and writes
+    of random spans of a deferred / armed mirror (numpy through the CPU view: faults, fetches,
+    read-ahead blocks and their tripwires, written pages), calls that upload the written pages,
+    run the in-place pass and defer again (the drop-in's deferred GenerateDoG), mirrored calls that
+    upload the written pages and copy everything back, explicit fetches and whole downloads — the
+    mirror must always show what a plain host array would, and the device what the same calls on a
+    plain array give (computed on a second context)."""
+    import ctypes
+
+    L = pkg.lib()
+    H = W = 512
+    S = 2
+    with pkg.PyramidContext(H, W, S=S) as a, pkg.PyramidContext(H, W, S=S) as ref_ctx:
+        n = L.gdp_image_floats(a._ctx)
+        a.set_input(oracle.lcg_image(H, W, 55), 0)
+        a.build()
+        a.sync()
+        dev = np.empty(n, np.float32)
+        assert L.gdp_download_image_raw(a._ctx, 0, dev.ctypes.data_as(ctypes.c_void_p)) == 0
+
+        def generate(x):  # the in-place pass on a plain array, on the second context
+            assert L.gdp_upload_image_raw(ref_ctx._ctx, 0, x.ctypes.data_as(ctypes.c_void_p)) == 0
+            assert L.gdp_generate_dog(ref_ctx._ctx, None) == 0
+            y = np.empty_like(x)
+            assert L.gdp_download_image_raw(ref_ctx._ctx, 0, y.ctypes.data_as(ctypes.c_void_p)) == 0
+            return y
+
+        hptr = ctypes.c_void_p()
+        assert L.gdp_host_alloc_tracked(n * 4, ctypes.byref(hptr)) == 0
+        try:
+            host = np.ctypeslib.as_array(ctypes.cast(hptr, ctypes.POINTER(ctypes.c_float)), shape=(n,))
+            assert L.gdp_download_image_raw(a._ctx, 0, hptr) == 0
+            assert L.gdp_host_arm(hptr) == 0
+            want = dev.copy()  # what the mirror must show
+            rng = np.random.default_rng(2026)
+            for case in range(6):
+                for step in range(40):
+                    k = rng.random()
+                    lo = int(rng.integers(0, n))
+                    span = int(rng.choice([1, 17, 1024, 40000, 300000]))
+                    hi = min(n, lo + span)
+                    if k < 0.30:  # a read of a span (sequential: faults, fetches, read-ahead)
+                        _assert_same(host[lo:hi], want[lo:hi], (case, step, "read"))
+                    elif k < 0.50:  # a write of a span
+                        v = rng.standard_normal(hi - lo).astype(np.float32)
+                        host[lo:hi] = v
+                        want[lo:hi] = v
+                    elif k < 0.68:  # the deferred call: written pages up, the pass, deferred again
+                        assert L.gdp_upload_image_written(a._ctx, 0, hptr) == 0
+                        assert L.gdp_generate_dog(a._ctx, None) == 0
+                        assert L.gdp_host_defer(a._ctx, 0, hptr) == 0
+                        want = generate(want)
+                    elif k < 0.80:  # the eager call: written pages up, the pass, everything back
+                        assert L.gdp_generate_dog_mirrored_written(a._ctx, 0, hptr) == 0
+                        want = generate(want)
+                    elif k < 0.88:
+                        assert L.gdp_host_fetch(hptr) == 0
+                    elif k < 0.94:  # the device copy back over everything (host edits discarded)
+                        assert L.gdp_upload_image_written(a._ctx, 0, hptr) == 0
+                        assert L.gdp_download_image_raw(a._ctx, 0, hptr) == 0
+                        assert L.gdp_host_arm(hptr) == 0
+                    else:  # a span read from several threads at once
+                        import threading
+
+                        got = np.empty(hi - lo, np.float32)
+                        parts = np.array_split(np.arange(lo, hi), 4)
+                        ts = [threading.Thread(target=lambda ix=ix: got.__setitem__(ix - lo, host[ix])) for ix in parts]
+                        for t in ts:
+                            t.start()
+                        for t in ts:
+                            t.join()
+                        _assert_same(got, want[lo:hi], (case, step, "threads"))
+                _assert_same(host, want, (case, "whole mirror"))
+                assert L.gdp_upload_image_written(a._ctx, 0, hptr) == 0
+                assert L.gdp_download_image_raw(a._ctx, 0, dev.ctypes.data_as(ctypes.c_void_p)) == 0
+                _assert_same(dev, want, (case, "device"))
+        finally:
+            L.gdp_host_free(hptr)
+
+
 @pytest.mark.parametrize("defer", [False, True])
 def test_cpp_class_random_edit_sequences_with_write_tracking(oracle, tmp_path, defer):
     """Seeded random op sequences on GaussPyramid_hip (examples/state_hip): host edits (single
