@@ -25,6 +25,12 @@ level; levels touched once stay in the refresh for the object's life
 reference rows, a dropped handle may still have been written).  GaussPyInit re-reads the CURRENT `data` (:80) and
 overwrites host edits, as the reference's refill does.  Levels never touched cost nothing.
 SyncDevice() uploads the edited levels on demand.
+GaussPyramid(img, len, S, defer=True) (round 6, as the C++ classes' DeferDownload): the levels are
+views of ONE write-tracked host mirror in the device layout; after a call its pages are fetched
+from the device only when first touched (sequential readers get the next block ahead), and the
+pages the caller writes are found by page faults — no snapshot comparison, no copy of levels the
+caller does not read.  Writing such an array to a file or socket straight from its memory (tofile,
+np.save, file.write) may fail with EFAULT on a page not fetched yet: copy it first (np.array(a)).
 
 Calling GenerateDoG() twice without GaussPyInit() re-filters the pyramid exactly like the
 reference's timing loop does (main.cpp:66-73).  The one behavioural difference is error
@@ -415,6 +421,22 @@ class PyramidContext:
             pass
 
 
+class _TrackedBuffer:
+    """gdp_host_alloc_tracked memory seen by numpy (GaussPyramid(defer=True)): arrays made from it
+    keep it alive, and it is freed when the last one goes."""
+
+    def __init__(self, nfloats):
+        p = ctypes.c_void_p()
+        check(lib().gdp_host_alloc_tracked(int(nfloats) * 4, ctypes.byref(p)))
+        self.ptr = p.value
+        self.__array_interface__ = {"shape": (int(nfloats),), "typestr": "<f4", "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().gdp_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
 class _LevelView:
     """GaussPy[o] -> list of S+3 level arrays, downloaded on first access after a change."""
 
@@ -434,10 +456,11 @@ class _LevelView:
 class GaussPyramid:
     """GPU mirror of `class GaussPyramid` (GuassDePyramid.h:11-29); see the module docstring."""
 
-    def __init__(self, img=None, len=None, S=2, device=0):  # noqa: A002  (reference argument name)
+    def __init__(self, img=None, len=None, S=2, device=0, defer=False):  # noqa: A002  (reference argument name)
         # GaussPyramid() (GuassDePyramid.h:31-34): empty object
         self.data = None
         self.initialized = False
+        self._defer = False
         if img is None:
             return
         length = int(len)
@@ -452,6 +475,13 @@ class GaussPyramid:
         self._raw = None  # one host buffer in the device's raw image layout; the levels are views
         self._fresh = False
         self.uploaded_levels = 0  # levels the last SyncDevice uploaded (0: the host held no edits)
+        if defer:
+            # deferred download (round 6, the C++ classes' DeferDownload): the levels are views of a
+            # write-tracked mirror (gdp_host_alloc_tracked) whose pages are fetched from the device
+            # when first touched after a call; edits are found by page faults, not by comparison
+            self._raw = np.asarray(_TrackedBuffer(lib().gdp_image_floats(self._ctx._ctx)))
+            self._defer = True
+            self.uploaded_bytes = 0
         self.GaussPyInit()  # :57
 
     # reference surface -------------------------------------------------------
@@ -498,7 +528,17 @@ class GaussPyramid:
     def SyncDevice(self):
         """Upload every level the caller obtained through GaussPy AND changed (its bits differ from
         the device's last copy) into the device pyramid; the next call processes the host contents.
-        Sets `uploaded_levels`."""
+        Sets `uploaded_levels`.  With defer=True: the pages written since the last call
+        (`uploaded_bytes`; `uploaded_levels` is 0 when nothing was written, else -1)."""
+        if self._defer:
+            w = ctypes.c_size_t()
+            written = w.value if lib().gdp_host_written_bytes(_ptr(self._raw), ctypes.byref(w)) == 0 else None
+            check(lib().gdp_upload_image_written(self._ctx._ctx, 0, _ptr(self._raw)), self._ctx._ctx)
+            self.uploaded_bytes = written
+            self.uploaded_levels = 0 if written == 0 else -1
+            if written != 0:
+                self._fresh = False
+            return
         n = 0
         for key, arr in self._cache.items():
             snap = self._snap[key]
@@ -513,6 +553,10 @@ class GaussPyramid:
     # helpers -----------------------------------------------------------------
     def _level(self, o, s):
         key = (o, s)
+        if key not in self._cache and self._defer:  # a view of the deferred mirror: fetched on touch
+            rows, cols = self._ctx.level_dims(o)[:2]
+            off = self._ctx.level_offset(0, o, s)
+            self._cache[key] = self._raw[off:off + rows * cols].reshape(rows, cols)
         if key not in self._cache:
             if self._raw is None:
                 self._raw = np.empty(lib().gdp_image_floats(self._ctx._ctx), np.float32)
@@ -529,7 +573,12 @@ class GaussPyramid:
     def _refresh(self):
         """After a device-side change: every touched level re-downloaded INTO its existing array,
         so handles the caller holds stay live (the reference's rows never move) — in one raw copy
-        of the image when the touched levels are at least half of its bytes, else level by level."""
+        of the image when the touched levels are at least half of its bytes, else level by level.
+        With defer=True: nothing is copied — the mirror is deferred (gdp_host_defer)."""
+        if self._defer:
+            self._ctx.sync()
+            check(lib().gdp_host_defer(self._ctx._ctx, 0, _ptr(self._raw)), self._ctx._ctx)
+            return
         if not self._cache:
             return
         self._ctx.sync()
@@ -559,8 +608,8 @@ class GaussPyramid_a512omp(GaussPyramid):
 
     counnt = 2  # GaussDePyramid-AVX512xOpenMP.h:18 (a global there; no effect on the GPU)
 
-    def __init__(self, img=None, len=None, S=2, device=0):  # noqa: A002
-        super().__init__(img, len, S, device)
+    def __init__(self, img=None, len=None, S=2, device=0, defer=False):  # noqa: A002
+        super().__init__(img, len, S, device, defer)
         if img is not None:
             self._ctx.set_window_centre("intlen")
 
@@ -597,8 +646,8 @@ class GaussPyramid_a512xp(GaussPyramid):
     semantics; GenerateDoG with that header's integer-length centre (:193, :218), GaussFilter with
     the serial float-halved one (:113-141)."""
 
-    def __init__(self, img=None, len=None, S=2, device=0):  # noqa: A002
-        super().__init__(img, len, S, device)
+    def __init__(self, img=None, len=None, S=2, device=0, defer=False):  # noqa: A002
+        super().__init__(img, len, S, device, defer)
         if img is not None:
             self._ctx.set_window_centre("intlen")
 

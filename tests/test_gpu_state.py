@@ -251,13 +251,15 @@ def test_cpp_mpitest_deferred_download(oracle, tmp_path):
                                                      "mpi"])
 
 
-def test_python_mirror_processes_host_edits(pkg, oracle):
+@pytest.mark.parametrize("defer", [False, True])
+def test_python_mirror_processes_host_edits(pkg, oracle, defer):
     """The Python GaussPyramid: writes through GaussPy[o][s] (element, row, whole level) and into
-    `data` are processed by the next call, like the reference's float**** and data copy."""
+    `data` are processed by the next call, like the reference's float**** and data copy (with
+    defer=True: on the deferred, write-tracked mirror)."""
     n, S = 100, 2
     O = oracle.octaves(n)
     img = oracle.lcg_image(n, n, 21)
-    g = pkg.GaussPyramid(img, n, S)
+    g = pkg.GaussPyramid(img, n, S, defer=defer)
     want = oracle.init_pyramid(img, S)
     lv = lambda p, o, s: oracle.levels(p, n, n, S, O)[(o, s)]  # noqa: E731
     g.GaussPy[0][1][5] *= np.float32(-3)
@@ -283,7 +285,8 @@ def test_python_mirror_processes_host_edits(pkg, oracle):
     g.close()
 
 
-def test_python_mirror_handles_stay_live_and_reads_upload_nothing(pkg, oracle):
+@pytest.mark.parametrize("defer", [False, True])
+def test_python_mirror_handles_stay_live_and_reads_upload_nothing(pkg, oracle, defer):
     """a GaussPy[o][s] array taken before a call is the same live array after it (the
     reference's rows never move): it reads the new contents, and writes through it — including
     ones __setitem__ never sees (a row view, a ufunc with out=) — are processed by the next call.
@@ -294,7 +297,7 @@ def test_python_mirror_handles_stay_live_and_reads_upload_nothing(pkg, oracle):
     n, S = 64, 2
     O = oracle.octaves(n)
     img = oracle.lcg_image(n, n, 41)
-    g = pkg.GaussPyramid(img, n, S)
+    g = pkg.GaussPyramid(img, n, S, defer=defer)
     lv = lambda p, o, s: oracle.levels(p, n, n, S, O)[(o, s)]  # noqa: E731
     a = g.GaussPy[0][0]  # taken before any call
     b = g.GaussPy[1][2]
@@ -312,7 +315,7 @@ def test_python_mirror_handles_stay_live_and_reads_upload_nothing(pkg, oracle):
     lv(want, 0, 0)[3] *= np.float32(-2)
     lv(want, 1, 2)[:] *= np.float32(0.5)
     g.GenerateDoG()
-    assert g.uploaded_levels == 2
+    assert g.uploaded_levels == (-1 if defer else 2)  # deferred mirror: pages, not levels, are tracked
     oracle.generate_dog(want, n, n, S, O)
     _assert_same(g.pyramid(), want, "edits through old handles processed")
     _assert_same(a, lv(want, 0, 0), "handle refreshed after the second call")
