@@ -433,7 +433,10 @@ class _TrackedBuffer:
 
     def __del__(self):
         if getattr(self, "ptr", None):
-            lib().gdp_host_free(ctypes.c_void_p(self.ptr))
+            try:
+                lib().gdp_host_free(ctypes.c_void_p(self.ptr))
+            except Exception:  # interpreter shutdown: the process unmaps it anyway
+                pass
             self.ptr = None
 
 
