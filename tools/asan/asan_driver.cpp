@@ -171,6 +171,15 @@ static void exercise(int H, int W, int S, int O, int B, int r0, int r1) {
             EXPECT(std::memcmp(t, dev.data(), raw.size() * 4) == 0);
             OK(gdp_upload_image_written(c, 0, t));
             OK(gdp_host_defer(c, 0, t));
+            {  // a sequential read of the whole mirror: growing blocks, read-ahead, tripwires
+                double sum = 0;
+                for (size_t i = 0; i < raw.size(); ++i) sum += t[i];
+                OK(gdp_host_deferred_stats(t, &st, &fb, &nf));
+                EXPECT(st == 0 && nf > 0 && sum == sum);
+                OK(gdp_download_image_raw(c, 0, dev.data()));
+                EXPECT(std::memcmp(t, dev.data(), raw.size() * 4) == 0);
+            }
+            OK(gdp_host_defer(c, 0, t));
             OK(gdp_download_image_raw(c, 0, t));  // ends the deferral
             OK(gdp_host_deferred_stats(t, &st, nullptr, nullptr));
             EXPECT(st == 0);
